@@ -1,0 +1,173 @@
+/*
+ * ykgpu.h — C-ABI of the MI355X (gfx950) renderer for the per-pixel sampling loop of
+ * yaito3014/UECRayTracing.  Plain C: no C++ or torch types cross this boundary.
+ *
+ * WHAT THIS REPLACES (reference file:line, /root/reference):
+ *   - the render loop   source.cpp:122-172  (for_each over (row,col) → transform_reduce over
+ *                       samples → image[y*W+x] = to_color3b(sum, spp))  → ykgpu_render*()
+ *   - yk::render<T>()   source.cpp:98-178   (returns image_t = std::array<color3b, W*H>,
+ *                       row-major, row 0 = top, RGB interleaved, stride 3W: source.cpp:70-71,
+ *                       224-226) → the caller-owned uint8_t[W*rows*3] output
+ *   - the world tuple   hittable_list.hpp:18-30 (objects in tuple order; the order defines
+ *                       rec.id, tie-breaking and scatter dispatch, hittable_list.hpp:32-73)
+ *                       → yk_sphere[] in the same order
+ *   - camera<T>         camera.hpp:14-38 (public origin / lower_left_corner / horizontal /
+ *                       vertical) → yk_camera
+ *   - constants         source.cpp:57-66 (image_width, samples_per_pixel, max_depth),
+ *                       t_min raytracer.hpp:27, seed source.cpp:118-120,154-159
+ *                       → yk_render_params
+ * The reference has no plugin/FFI layer of its own: these are the entry points a
+ * C++ caller (our drop-in `raytrace`, or the reference's own source.cpp through
+ * include/yk/ykgpu_bridge.hpp) binds.  See INTEGRATION.md.
+ *
+ * Conventions: every function returns YK_OK (0) or a YK_ERR_* code; the message of the last
+ * failure on the calling thread is ykgpu_last_error().  No exceptions cross the ABI.  A context
+ * owns one device's memory and stream; calls on one context are synchronous unless named
+ * *_async and are NOT reentrant per context (the reference calls render() once from main).
+ */
+#ifndef YKGPU_H
+#define YKGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YKGPU_ABI_VERSION 1u
+
+/* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
+ * METAL with fuzz > 0 and DIELECTRIC are extensions needed by BASELINE configs 2-5 (no
+ * reference oracle exists for them: parity unpinned). */
+enum { YK_MATERIAL_LAMBERTIAN = 0, YK_MATERIAL_METAL = 1, YK_MATERIAL_DIELECTRIC = 2 };
+
+/* Arithmetic of the per-sample path.  FP64 reproduces the reference (T = double,
+ * source.cpp:98) bit for bit. */
+enum { YK_PRECISION_FP64 = 0 };
+
+/* Random stream.  MT19937 = yk::mt19937 (random.hpp:148-151) seeded per sample with
+ * seed0 + (y*W + x)*spp + s in uint32 arithmetic (source.cpp:154-158). */
+enum { YK_RNG_MT19937 = 0 };
+
+/* yk_render_params.flags */
+enum {
+  YK_FLAG_COUNT_WORK = 1u /* count segments / sphere tests (ykgpu_get_stats) */
+};
+
+enum {
+  YK_OK = 0,
+  YK_ERR_INVALID = 1,     /* bad argument (null pointer, zero size, row range outside image) */
+  YK_ERR_DEVICE = 2,      /* HIP runtime failure / no device                                 */
+  YK_ERR_NOMEM = 3,       /* device allocation failed                                        */
+  YK_ERR_UNSUPPORTED = 4, /* a mode this build does not implement                            */
+  YK_ERR_NO_SCENE = 5     /* render before ykgpu_set_scene                                   */
+};
+
+/* One sphere<T, M> of the world tuple (sphere.hpp:16-23), in tuple order. 80 bytes. */
+typedef struct yk_sphere {
+  double center[3];
+  double radius;    /* may be negative (hollow dielectric shell, extension)              */
+  double albedo[3]; /* lambertian / metal albedo (material.hpp:39,57)                    */
+  double fuzz;      /* metal only; 0 = the reference's metal (no random draw)            */
+  double ior;       /* dielectric only                                                    */
+  uint32_t material;/* YK_MATERIAL_*                                                      */
+  uint32_t reserved;
+} yk_sphere;
+
+/* camera<T> public members (camera.hpp:34-37) plus the thin-lens basis of the defocus
+ * extension.  lens_radius == 0 gives exactly the reference's get_ray (camera.hpp:29-32). */
+typedef struct yk_camera {
+  double origin[3];
+  double lower_left_corner[3];
+  double horizontal[3];
+  double vertical[3];
+  double lens_u[3];
+  double lens_v[3];
+  double lens_radius;
+} yk_camera;
+
+typedef struct yk_render_params {
+  uint32_t image_width;       /* W  (constants::image_width, source.cpp:60)            */
+  uint32_t image_height;      /* H  (source.cpp:61-62: uint32(W / (16/9)))             */
+  uint32_t samples_per_pixel; /* spp (source.cpp:63)                                   */
+  uint32_t max_depth;         /* source.cpp:64                                          */
+  uint32_t seed0;             /* constexpr_seed (source.cpp:118-120); 404 = "00:00:00"  */
+  uint32_t row_begin;         /* rendered rows: row_begin + i*row_stride, i < row_count */
+  uint32_t row_count;         /*   (a tile of the image; the whole image: 0, H, 1)      */
+  uint32_t row_stride;
+  uint32_t precision;         /* YK_PRECISION_*                                         */
+  uint32_t rng;               /* YK_RNG_*                                               */
+  uint32_t flags;             /* YK_FLAG_*                                              */
+  uint32_t reserved;
+  double t_min;               /* 0.001 in the reference (raytracer.hpp:27)              */
+} yk_render_params;
+
+typedef struct yk_render_stats {
+  double kernel_ms;        /* path-tracing kernel(s), HIP events on the render stream  */
+  double resolve_ms;       /* per-pixel sum + to_color3b kernel                        */
+  double total_ms;         /* whole call, host wall clock                              */
+  uint64_t samples;        /* primary samples rendered                                 */
+  uint64_t segments;       /* ray_color calls that ran a closest-hit (flag COUNT_WORK) */
+  uint64_t sphere_tests;   /* ray-sphere discriminant tests (flag COUNT_WORK)          */
+  uint64_t sqrt_calls;     /* Newton square roots on hit candidates (flag COUNT_WORK)  */
+  uint64_t mt_fallbacks;   /* samples that needed the full 624-word MT state           */
+  uint32_t launches;       /* path-tracing launches in the call                        */
+  uint32_t grid_blocks;    /* persistent grid size                                     */
+} yk_render_stats;
+
+typedef struct ykgpu_context ykgpu_context;
+
+uint32_t ykgpu_abi_version(void);
+const char* ykgpu_last_error(void);
+
+int ykgpu_device_count(int* count);
+int ykgpu_context_create(int device, ykgpu_context** out);
+int ykgpu_context_destroy(ykgpu_context* ctx);
+
+/* Uploads the world (tuple order) and the camera to HBM.  Replaces building `world` and `cam`
+ * inside render() (source.cpp:100-112). */
+int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count,
+                    const yk_camera* camera);
+
+/* The render loop (source.cpp:122-172) for the rows named by params, synchronous, into a
+ * caller-owned host buffer of row_count * W * 3 bytes laid out like image_t. */
+int ykgpu_render(ykgpu_context* ctx, const yk_render_params* params, uint8_t* rgb_host);
+
+/* Same, into device memory (row_count * W * 3 bytes on ctx's device), enqueued on `stream`
+ * (a hipStream_t; NULL = the context's own stream).  Does not synchronise. */
+int ykgpu_render_async(ykgpu_context* ctx, const yk_render_params* params, void* rgb_device,
+                       void* stream);
+
+/* Diagnostics: the per-pixel colour sum before to_color3b (source.cpp:137-167), 3 doubles per
+ * pixel, row_count * W * 3 doubles, host buffer. */
+int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* params, double* sums_host);
+
+/* Statistics of the last render on this context. */
+int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out);
+
+/* ---- host-side scene helpers (no device needed) ---------------------------------------- */
+
+/* camera<double>{} of camera.hpp:16-27 (16:9, viewport height 2, focal length 1, origin 0). */
+int yk_camera_reference(yk_camera* out);
+
+/* Positionable thin-lens camera (extension for configs 2-5). vfov in degrees. */
+int yk_camera_look(yk_camera* out, const double lookfrom[3], const double lookat[3],
+                   const double vup[3], double vfov_deg, double aspect, double aperture,
+                   double focus_dist);
+
+/* Named scenes: "ref4" (source.cpp:103-112), "lambert3", "mixed12", "rtiow5" (config 2),
+ * "final" (RTIOW final scene, ~488 spheres, configs 3/4), "glass" (dielectric-heavy, config 5).
+ * `seed` drives the random generators of "final" / "glass".  Writes up to `capacity` spheres,
+ * the count to *count and the scene's camera to *camera (either may be NULL to query). */
+int yk_scene_build(const char* name, uint32_t seed, yk_sphere* spheres, uint32_t capacity,
+                   uint32_t* count, yk_camera* camera);
+
+/* Image height of the reference for a width: uint32(W / (16.0/9.0)) (source.cpp:61-62). */
+uint32_t yk_image_height_for(uint32_t width);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* YKGPU_H */

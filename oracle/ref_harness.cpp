@@ -1,0 +1,238 @@
+// oracle/ref_harness.cpp — TEST INFRASTRUCTURE ONLY (never shipped, never measured).
+//
+// A driver of our own that #includes the reference's headers IN PLACE (-I/root/reference,
+// nothing copied) and runs the reference's per-pixel loop deterministically, so that golden
+// fixtures can be generated from the reference itself.  It is compiled by oracle/Makefile into
+// oracle/_ref/ (git-ignored) only when /root/reference exists.
+//
+// The loop below has the shape of /root/reference/source.cpp:122-172 with the seed that the
+// reference's constexpr build uses (source.cpp:118-120,154-158):
+//     mt19937 gen(seed0 + (y*W + x)*spp + s)     (uint32 arithmetic, wraps mod 2^32)
+// instead of std::random_device (source.cpp:159), which is what makes the output reproducible.
+// The per-pixel sum is the same std::transform_reduce over iota(0,spp) (source.cpp:137-167) and
+// the quantisation is a call-for-call restatement of to_color3b (source.cpp:73-83) built from the
+// reference's own color3 / math::sqrt.
+//
+// Scenes are compile-time hittable_list tuples made only of reference types (sphere, lambertian,
+// metal; yk/sphere.hpp, yk/material.hpp):
+//   ref4     — source.cpp:103-112 verbatim values (the reference's only scene)
+//   lambert3 — the same spheres with every material lambertian (BASELINE config 1 wording)
+//   mixed12  — 12 spheres incl. an exact duplicate (tie-break rule of hittable_list.hpp:32-58)
+//   walls2   — two facing lambertian walls: long paths (RNG draws past 227 / 624)
+//
+// Modes:
+//   ref_harness render  <scene> W H spp depth seed0 out.rgb [out.sums]
+//   ref_harness samples <scene> W H spp depth seed0 y x s [y x s ...]   (per-sample colours, hex)
+//   ref_harness kat                                                   (RNG / sqrt / canonical KATs)
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <numeric>
+#include <ranges>
+#include <string>
+#include <vector>
+
+#include "yk/camera.hpp"
+#include "yk/color.hpp"
+#include "yk/config.hpp"
+#include "yk/hittable.hpp"
+#include "yk/hittable_list.hpp"
+#include "yk/material.hpp"
+#include "yk/math.hpp"
+#include "yk/random.hpp"
+#include "yk/ray.hpp"
+#include "yk/raytracer.hpp"
+#include "yk/sphere.hpp"
+#include "yk/vec3.hpp"
+
+namespace {
+
+using P = yk::pos3<double, yk::world_tag>;
+using L = yk::lambertian<double>;
+using M = yk::metal<double>;
+
+// Counts u32 draws so fixtures can record stream consumption (values are untouched).
+struct counting_gen {
+  yk::mt19937* g;
+  std::uint64_t n = 0;
+  using result_type = yk::mt19937::result_type;
+  static constexpr result_type min() { return yk::mt19937::min(); }
+  static constexpr result_type max() { return yk::mt19937::max(); }
+  result_type operator()() { ++n; return (*g)(); }
+};
+
+auto scene_ref4() {
+  return yk::hittable_list<double>{}
+      .add(yk::sphere(P(0, 0, -1), 0.5, L({0.7, 0.3, 0.3})))
+      .add(yk::sphere(P(0, -100.5, -1), 100.0, L({0.8, 0.8, 0.0})))
+      .add(yk::sphere(P(-1.0, 0.0, -1.0), 0.5, M({0.8, 0.8, 0.8})))
+      .add(yk::sphere(P(1.0, 0.0, -1.0), 0.5, M({0.8, 0.6, 0.2})));
+}
+
+auto scene_lambert3() {
+  return yk::hittable_list<double>{}
+      .add(yk::sphere(P(0, 0, -1), 0.5, L({0.7, 0.3, 0.3})))
+      .add(yk::sphere(P(0, -100.5, -1), 100.0, L({0.8, 0.8, 0.0})))
+      .add(yk::sphere(P(-1.0, 0.0, -1.0), 0.5, L({0.8, 0.8, 0.8})));
+}
+
+auto scene_mixed12() {
+  return yk::hittable_list<double>{}
+      .add(yk::sphere(P(0, -100.5, -1), 100.0, L({0.8, 0.8, 0.0})))
+      .add(yk::sphere(P(0, 0, -1), 0.5, L({0.1, 0.2, 0.5})))
+      .add(yk::sphere(P(-1.0, 0.0, -1.0), 0.5, M({0.8, 0.8, 0.8})))
+      .add(yk::sphere(P(1.0, 0.0, -1.0), 0.5, M({0.8, 0.6, 0.2})))
+      .add(yk::sphere(P(0, 0, -1), 0.5, M({0.9, 0.9, 0.9})))
+      .add(yk::sphere(P(-0.5, 0.6, -1.5), 0.3, L({0.9, 0.1, 0.1})))
+      .add(yk::sphere(P(0.5, 0.6, -1.5), 0.3, M({0.2, 0.9, 0.2})))
+      .add(yk::sphere(P(0, -0.3, -0.6), 0.15, L({0.2, 0.2, 0.9})))
+      .add(yk::sphere(P(0.3, 0.1, -0.45), 0.1, M({0.95, 0.95, 0.95})))
+      .add(yk::sphere(P(-0.35, -0.35, -0.7), 0.12, L({0.5, 0.9, 0.5})))
+      .add(yk::sphere(P(0, 1.2, -2.5), 0.6, L({0.7, 0.7, 0.7})))
+      .add(yk::sphere(P(1.0, 0.0, -1.0), 0.25, L({0.3, 0.3, 0.3})));
+}
+
+// two huge facing lambertian walls: long bounce chains (draws > 227 and > 624 at depth 200)
+auto scene_walls2() {
+  return yk::hittable_list<double>{}
+      .add(yk::sphere(P(0, -300.5, -1), 300.0, L({0.9, 0.85, 0.8})))
+      .add(yk::sphere(P(0, 300.5, -1), 300.0, L({0.8, 0.9, 0.95})));
+}
+
+struct job {
+  std::uint32_t W, H, spp, depth, seed0;
+};
+
+template <class World>
+yk::color3d sample_color(const World& world, const job& j, std::uint32_t y, std::uint32_t x,
+                         std::uint32_t s, std::uint64_t* draws) {
+  const yk::raytracer<double, double> tracer = {};
+  const yk::camera<double> cam = {};
+  yk::mt19937 g(j.seed0 + (y * j.W + x) * j.spp + s);
+  counting_gen gen{&g};
+  yk::uniform_real_distribution<double> dist(0, 1);
+  auto u = (x + dist(gen)) / j.W;
+  auto v = (j.H - y - 1 + dist(gen)) / j.H;
+  auto c = tracer.ray_color(cam.get_ray(u, v), world, j.depth, gen);
+  if (draws) *draws = gen.n;
+  return c;
+}
+
+template <class World>
+int render(const World& world, const job& j, const char* out_rgb, const char* out_sums) {
+  std::vector<unsigned char> rgb(std::size_t(j.W) * j.H * 3);
+  std::vector<double> sums(std::size_t(j.W) * j.H * 3);
+  for (std::uint32_t y = 0; y < j.H; ++y) {
+    for (std::uint32_t x = 0; x < j.W; ++x) {
+      auto iota = std::views::iota(0u, j.spp);
+      yk::color3d pc = std::transform_reduce(
+          iota.begin(), iota.end(), yk::color3d(0, 0, 0), std::plus{},
+          [&](auto s) { return sample_color(world, j, y, x, s, nullptr); });
+      const std::size_t i = std::size_t(y) * j.W + x;
+      sums[3 * i + 0] = pc.r;
+      sums[3 * i + 1] = pc.g;
+      sums[3 * i + 2] = pc.b;
+      // to_color3b, source.cpp:73-83
+      auto [r, g, b] = pc / j.spp;
+      yk::color3d c = {.r = yk::math::sqrt(r), .g = yk::math::sqrt(g), .b = yk::math::sqrt(b)};
+      auto q = (c.clamped(0.0, 0.999) * 256).template to<std::uint8_t>();
+      rgb[3 * i + 0] = q.r;
+      rgb[3 * i + 1] = q.g;
+      rgb[3 * i + 2] = q.b;
+    }
+  }
+  FILE* f = std::fopen(out_rgb, "wb");
+  if (!f) return 1;
+  std::fwrite(rgb.data(), 1, rgb.size(), f);
+  std::fclose(f);
+  if (out_sums) {
+    f = std::fopen(out_sums, "wb");
+    if (!f) return 1;
+    std::fwrite(sums.data(), sizeof(double), sums.size(), f);
+    std::fclose(f);
+  }
+  return 0;
+}
+
+template <class World>
+int samples(const World& world, const job& j, int argc, char** argv) {
+  std::printf("[\n");
+  for (int k = 0; k + 2 < argc; k += 3) {
+    std::uint32_t y = std::strtoul(argv[k], nullptr, 10);
+    std::uint32_t x = std::strtoul(argv[k + 1], nullptr, 10);
+    std::uint32_t s = std::strtoul(argv[k + 2], nullptr, 10);
+    std::uint64_t n = 0;
+    auto c = sample_color(world, j, y, x, s, &n);
+    std::printf("  {\"y\": %u, \"x\": %u, \"s\": %u, \"draws\": %llu, \"rgb\": [\"%a\", \"%a\", \"%a\"]}%s\n",
+                y, x, s, (unsigned long long)n, c.r, c.g, c.b, (k + 5 < argc) ? "," : "");
+  }
+  std::printf("]\n");
+  return 0;
+}
+
+int kat() {
+  std::printf("{\n  \"mt19937\": {\n");
+  const std::uint32_t seeds[] = {5489u, 404u, 0u, 1u, 4294967295u, 123456789u};
+  for (std::size_t k = 0; k < sizeof(seeds) / sizeof(seeds[0]); ++k) {
+    yk::mt19937 g(seeds[k]);
+    std::printf("    \"%u\": [", seeds[k]);
+    // 1300 outputs: crosses the lazy-cursor limit (227), one full re-twist (624) and a second.
+    for (int i = 0; i < 1300; ++i) std::printf("%s%llu", i ? ", " : "", (unsigned long long)g());
+    std::printf("]%s\n", (k + 1 < sizeof(seeds) / sizeof(seeds[0])) ? "," : "");
+  }
+  std::printf("  },\n  \"canonical01\": {\n");
+  for (std::size_t k = 0; k < sizeof(seeds) / sizeof(seeds[0]); ++k) {
+    yk::mt19937 g(seeds[k]);
+    yk::uniform_real_distribution<double> d01(0, 1), dpm(-1, 1);
+    std::printf("    \"%u\": [", seeds[k]);
+    for (int i = 0; i < 64; ++i) {
+      double v = (i % 3 == 2) ? dpm(g) : d01(g);  // pattern 0,1 / -1,1 mixes both ranges
+      std::printf("%s\"%a\"", i ? ", " : "", v);
+    }
+    std::printf("]%s\n", (k + 1 < sizeof(seeds) / sizeof(seeds[0])) ? "," : "");
+  }
+  std::printf("  },\n  \"newton_sqrt\": [");
+  // deterministic spread of inputs (LCG-scrambled mantissas over many binades) plus edges
+  std::vector<double> xs = {0.0, 1.0, 2.0, 4.0, 0.25, 1e-300, 5e-324, 1e300, 3.0, 0.999, 1e-8};
+  std::uint64_t st = 0x9E3779B97F4A7C15ull;
+  for (int i = 0; i < 500; ++i) {
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    double m = 1.0 + double(st >> 11) * 0x1p-53;
+    int e = int((st >> 3) % 60) - 30;
+    xs.push_back(std::ldexp(m, e));
+  }
+  for (std::size_t i = 0; i < xs.size(); ++i)
+    std::printf("%s[\"%a\", \"%a\"]", i ? ", " : "", xs[i], yk::math::sqrt(xs[i]));
+  std::printf("]\n}\n");
+  return 0;
+}
+
+template <class World>
+int dispatch_world(const World& w, const char* mode, const job& j, int argc, char** argv) {
+  if (!std::strcmp(mode, "render")) return render(w, j, argv[0], argc > 1 ? argv[1] : nullptr);
+  return samples(w, j, argc, argv);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc >= 2 && !std::strcmp(argv[1], "kat")) return kat();
+  if (argc < 9) {
+    std::fprintf(stderr, "usage: %s render|samples scene W H spp depth seed0 ...\n", argv[0]);
+    return 2;
+  }
+  job j{(std::uint32_t)std::strtoul(argv[3], nullptr, 10), (std::uint32_t)std::strtoul(argv[4], nullptr, 10),
+        (std::uint32_t)std::strtoul(argv[5], nullptr, 10), (std::uint32_t)std::strtoul(argv[6], nullptr, 10),
+        (std::uint32_t)std::strtoul(argv[7], nullptr, 10)};
+  const std::string scene = argv[2];
+  if (scene == "ref4") return dispatch_world(scene_ref4(), argv[1], j, argc - 8, argv + 8);
+  if (scene == "lambert3") return dispatch_world(scene_lambert3(), argv[1], j, argc - 8, argv + 8);
+  if (scene == "mixed12") return dispatch_world(scene_mixed12(), argv[1], j, argc - 8, argv + 8);
+  if (scene == "walls2") return dispatch_world(scene_walls2(), argv[1], j, argc - 8, argv + 8);
+  std::fprintf(stderr, "unknown scene %s\n", scene.c_str());
+  return 2;
+}

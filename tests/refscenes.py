@@ -1,0 +1,63 @@
+"""Reference-expressible scenes, written out independently of the product's C++ scene builder.
+
+Values are those of /root/reference/source.cpp:103-112 ("ref4") and of the scenes
+oracle/ref_harness.cpp renders through the reference headers (same names).  Used by the oracle
+tests (no product code involved) and to cross-check the product's yk_scene_build().
+"""
+from uecraytracing_amd.records import Camera, D3, lambertian, metal
+
+
+def reference_camera() -> Camera:
+    """camera<double>{} — camera.hpp:16-27, evaluated in the same order."""
+    aspect_ratio = 16.0 / 9.0
+    viewport_height = 2.0
+    viewport_width = aspect_ratio * viewport_height
+    focal_length = 1.0
+    h = (viewport_width, 0.0, 0.0)
+    v = (0.0, viewport_height, 0.0)
+    llc = tuple(((0.0 - h[i] / 2) - v[i] / 2) - (0.0, 0.0, focal_length)[i] for i in range(3))
+    return Camera(D3(0.0, 0.0, 0.0), D3(*llc), D3(*h), D3(*v), D3(0, 0, 0), D3(0, 0, 0), 0.0)
+
+
+def ref4():
+    return [
+        lambertian((0, 0, -1), 0.5, (0.7, 0.3, 0.3)),
+        lambertian((0, -100.5, -1), 100.0, (0.8, 0.8, 0.0)),
+        metal((-1.0, 0.0, -1.0), 0.5, (0.8, 0.8, 0.8)),
+        metal((1.0, 0.0, -1.0), 0.5, (0.8, 0.6, 0.2)),
+    ]
+
+
+def lambert3():
+    return [
+        lambertian((0, 0, -1), 0.5, (0.7, 0.3, 0.3)),
+        lambertian((0, -100.5, -1), 100.0, (0.8, 0.8, 0.0)),
+        lambertian((-1.0, 0.0, -1.0), 0.5, (0.8, 0.8, 0.8)),
+    ]
+
+
+def mixed12():
+    return [
+        lambertian((0, -100.5, -1), 100.0, (0.8, 0.8, 0.0)),
+        lambertian((0, 0, -1), 0.5, (0.1, 0.2, 0.5)),
+        metal((-1.0, 0.0, -1.0), 0.5, (0.8, 0.8, 0.8)),
+        metal((1.0, 0.0, -1.0), 0.5, (0.8, 0.6, 0.2)),
+        metal((0, 0, -1), 0.5, (0.9, 0.9, 0.9)),
+        lambertian((-0.5, 0.6, -1.5), 0.3, (0.9, 0.1, 0.1)),
+        metal((0.5, 0.6, -1.5), 0.3, (0.2, 0.9, 0.2)),
+        lambertian((0, -0.3, -0.6), 0.15, (0.2, 0.2, 0.9)),
+        metal((0.3, 0.1, -0.45), 0.1, (0.95, 0.95, 0.95)),
+        lambertian((-0.35, -0.35, -0.7), 0.12, (0.5, 0.9, 0.5)),
+        lambertian((0, 1.2, -2.5), 0.6, (0.7, 0.7, 0.7)),
+        lambertian((1.0, 0.0, -1.0), 0.25, (0.3, 0.3, 0.3)),
+    ]
+
+
+def walls2():
+    return [
+        lambertian((0, -300.5, -1), 300.0, (0.9, 0.85, 0.8)),
+        lambertian((0, 300.5, -1), 300.0, (0.8, 0.9, 0.95)),
+    ]
+
+
+SCENES = {"ref4": ref4, "lambert3": lambert3, "mixed12": mixed12, "walls2": walls2}

@@ -1,0 +1,91 @@
+"""Pins the CPU oracle (oracle/yk_oracle.c) to fixtures generated from the reference itself.
+
+Every assertion is bit-exact: RGB8 bytes, per-pixel float64 sums (bytes or sha256), per-sample
+colours (hex doubles) and RNG draw counts, mt19937 outputs, canonical doubles, Newton sqrt.
+"""
+import numpy as np
+import pytest
+
+import golden_data
+import oracle_lib
+import refscenes
+from uecraytracing_amd.records import make_params
+
+MAN = golden_data.manifest()
+CASES = MAN["cases"]
+
+
+def test_mt19937_kat():
+    kat = golden_data.kat()["mt19937"]
+    assert oracle_lib.mt19937(5489, 1)[0] == 3499211612  # random.hpp default seed, std KAT
+    for seed, outs in kat.items():
+        assert oracle_lib.mt19937(int(seed), len(outs)) == outs, seed
+
+
+def test_canonical_kat():
+    for seed, vals in golden_data.kat()["canonical01"].items():
+        got = oracle_lib.canonical_pattern(int(seed), len(vals))
+        assert [g.hex() for g in got] == [float.fromhex(v).hex() for v in vals], seed
+
+
+def test_newton_sqrt_kat():
+    for x, y in golden_data.kat()["newton_sqrt"]:
+        assert oracle_lib.newton_sqrt(float.fromhex(x)).hex() == float.fromhex(y).hex(), x
+
+
+def test_constexpr_build_of_source_cpp():
+    e = MAN["constexpr_build"]
+    rgb, _, _, _ = oracle_lib.render(refscenes.ref4(), refscenes.reference_camera(),
+                                     make_params(16, 9, 2, 50, 404))
+    assert golden_data.sha(rgb) == e["rgb_sha256"]
+
+
+@pytest.mark.parametrize("entry", CASES, ids=[c["name"] for c in CASES])
+def test_render_matches_reference(entry):
+    if entry["W"] * entry["H"] * entry["spp"] > 300_000:
+        pytest.skip("large case covered by test_render_matches_reference_large")
+    _check_case(entry)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("entry", [c for c in CASES if c["W"] * c["H"] * c["spp"] > 300_000],
+                         ids=lambda c: c["name"])
+def test_render_matches_reference_large(entry):
+    _check_case(entry)
+
+
+def _check_case(entry):
+    sph = refscenes.SCENES[entry["scene"]]()
+    p = make_params(entry["W"], entry["H"], entry["spp"], entry["depth"], entry["seed0"])
+    rgb, sums, _, _ = oracle_lib.render(sph, refscenes.reference_camera(), p, want_sums=True)
+    np.testing.assert_array_equal(rgb, golden_data.rgb(entry))
+    assert golden_data.sha(sums) == entry["sums_sha256"]
+    ref_sums = golden_data.sums(entry)
+    if ref_sums is not None:
+        assert sums.tobytes() == ref_sums.tobytes()
+
+
+@pytest.mark.parametrize("scene", sorted(MAN["samples"]))
+def test_per_sample_paths(scene):
+    spec = MAN["samples"][scene]
+    sph, cam = refscenes.SCENES[scene](), refscenes.reference_camera()
+    p = make_params(spec["W"], spec["H"], spec["spp"], spec["depth"], spec["seed0"])
+    for pt in spec["points"]:
+        col, draws = oracle_lib.sample(sph, cam, p, pt["y"], pt["x"], pt["s"])
+        assert draws == pt["draws"], pt
+        assert [c.hex() for c in col] == [float.fromhex(v).hex() for v in pt["rgb"]], pt
+
+
+def test_row_tiles_concatenate_to_the_image():
+    """Cyclic row tiles (the multi-GPU partition) reassemble into the 1-tile image."""
+    e = next(c for c in CASES if c["name"] == "ref4_33x17x5_d50_s7")
+    sph, cam = refscenes.ref4(), refscenes.reference_camera()
+    full = golden_data.rgb(e)
+    for n in (2, 3, 4):
+        out = np.zeros_like(full)
+        for r in range(n):
+            rows = len(range(r, e["H"], n))
+            p = make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], rows=(r, rows, n))
+            tile, _, _, _ = oracle_lib.render(sph, cam, p)
+            out[r::n] = tile
+        np.testing.assert_array_equal(out, full)
