@@ -1,0 +1,85 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports every entry point
+include/ykgpu.h declares, its host-side scene helpers reproduce the reference's scene values,
+and the product has no CPU fallback (rendering without a GPU fails loudly)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import refscenes
+import uecraytracing_amd as yk
+from uecraytracing_amd import records
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                      "ykgpu.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(yk\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    assert set(names) == set(yk.EXPORTS), names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = yk.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.ykgpu_abi_version() == 1
+
+
+def test_reference_camera_matches_camera_hpp():
+    assert yk.reference_camera().as_tuple() == refscenes.reference_camera().as_tuple()
+
+
+@pytest.mark.parametrize("name", sorted(refscenes.SCENES))
+def test_scene_builder_matches_reference_values(name):
+    arr, cam = yk.build_scene(name)
+    want = refscenes.SCENES[name]()
+    assert [s.as_tuple() for s in arr] == [s.as_tuple() for s in want]
+    assert cam.as_tuple() == refscenes.reference_camera().as_tuple()
+
+
+def test_extension_scenes_are_deterministic():
+    a, ca = yk.build_scene("final", 42)
+    b, cb = yk.build_scene("final", 42)
+    c, _ = yk.build_scene("final", 43)
+    assert 400 < len(a) < 490
+    assert [s.as_tuple() for s in a] == [s.as_tuple() for s in b]
+    assert [s.as_tuple() for s in a] != [s.as_tuple() for s in c]
+    assert ca.lens_radius == 0.05 and ca.as_tuple() == cb.as_tuple()
+    kinds = {s.material for s in a}
+    assert kinds == {records.MATERIAL_LAMBERTIAN, records.MATERIAL_METAL, records.MATERIAL_DIELECTRIC}
+    g, _ = yk.build_scene("glass", 42)
+    frac = sum(s.material == records.MATERIAL_DIELECTRIC for s in g) / len(g)
+    assert frac > 0.4
+
+
+def test_unknown_scene_is_an_error():
+    with pytest.raises(yk.YkError):
+        yk.build_scene("nope")
+
+
+def test_image_height_matches_source_cpp():
+    lib = yk.load_library()
+    for w in (16, 200, 400, 800, 1920, 3840):
+        assert lib.yk_image_height_for(w) == records.image_height_for(w)
+    assert records.image_height_for(200) == 112 and records.image_height_for(1920) == 1080
+
+
+def test_no_cpu_fallback_without_a_gpu():
+    if yk.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(yk.YkError):
+        yk.Renderer(0)
+
+
+def test_invalid_arguments_are_reported():
+    lib = yk.load_library()
+    assert lib.ykgpu_context_create(0, None) == 1
+    assert b"null" in lib.ykgpu_last_error()
+    assert lib.ykgpu_set_scene(None, None, 0, None) == 1

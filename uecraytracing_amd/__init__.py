@@ -1,0 +1,165 @@
+"""uecraytracing_amd — MI355X (gfx950) renderer for the per-pixel sampling loop of
+yaito3014/UECRayTracing.
+
+The product is the C-ABI library ``uecraytracing_amd/lib/libykgpu.so`` (include/ykgpu.h) and the
+drop-in CLI ``uecraytracing_amd/lib/raytrace``.  This module is a thin ctypes view of that
+library for tests and the benchmark: it has NO fallback — if the library or a GPU is missing,
+every render raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import records
+from .records import Camera, RenderParams, RenderStats, Sphere, make_params, sphere_array
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libykgpu.so")
+CLI_PATH = os.path.join(LIB_DIR, "raytrace")
+
+EXPORTS = (
+    "ykgpu_abi_version", "ykgpu_last_error", "ykgpu_device_count", "ykgpu_context_create",
+    "ykgpu_context_destroy", "ykgpu_set_scene", "ykgpu_render", "ykgpu_render_async",
+    "ykgpu_render_sums", "ykgpu_get_stats", "yk_camera_reference", "yk_camera_look",
+    "yk_scene_build", "yk_image_height_for",
+)
+
+_lib = None
+
+
+class YkError(RuntimeError):
+    pass
+
+
+def load_library():
+    """Loads libykgpu.so (built by __graft_entry__.build / `make -C uecraytracing_amd/csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise YkError(f"{LIB_PATH} is missing: build it with `make -C uecraytracing_amd/csrc` "
+                      "(there is no CPU fallback)")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64/libhsa-runtime64
+    # (soname libamdhip64.so.7, like /opt/rocm's).  If torch is importable it is loaded FIRST
+    # so that libykgpu.so binds to the already-loaded runtime instead of pulling in a second
+    # copy, which would leave whichever initialises second without a GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(LIB_PATH)
+    P, c = ctypes.POINTER, ctypes
+    sig = {
+        "ykgpu_abi_version": ([], c.c_uint32),
+        "ykgpu_last_error": ([], c.c_char_p),
+        "ykgpu_device_count": ([P(c.c_int)], c.c_int),
+        "ykgpu_context_create": ([c.c_int, P(c.c_void_p)], c.c_int),
+        "ykgpu_context_destroy": ([c.c_void_p], c.c_int),
+        "ykgpu_set_scene": ([c.c_void_p, P(Sphere), c.c_uint32, P(Camera)], c.c_int),
+        "ykgpu_render": ([c.c_void_p, P(RenderParams), c.c_void_p], c.c_int),
+        "ykgpu_render_async": ([c.c_void_p, P(RenderParams), c.c_void_p, c.c_void_p], c.c_int),
+        "ykgpu_render_sums": ([c.c_void_p, P(RenderParams), c.c_void_p], c.c_int),
+        "ykgpu_get_stats": ([c.c_void_p, P(RenderStats)], c.c_int),
+        "yk_camera_reference": ([P(Camera)], c.c_int),
+        "yk_camera_look": ([P(Camera), P(c.c_double), P(c.c_double), P(c.c_double), c.c_double,
+                            c.c_double, c.c_double, c.c_double], c.c_int),
+        "yk_scene_build": ([c.c_char_p, c.c_uint32, P(Sphere), c.c_uint32, P(c.c_uint32),
+                            P(Camera)], c.c_int),
+        "yk_image_height_for": ([c.c_uint32], c.c_uint32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes, f.restype = args, res
+    if lib.ykgpu_abi_version() != 1:
+        raise YkError("ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != 0:
+        msg = load_library().ykgpu_last_error().decode(errors="replace")
+        raise YkError(f"{records.ERRORS.get(rc, rc)}: {msg}")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = load_library().ykgpu_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def reference_camera() -> Camera:
+    cam = Camera()
+    _check(load_library().yk_camera_reference(ctypes.byref(cam)))
+    return cam
+
+
+def build_scene(name: str, seed: int = 0):
+    """Named scenes of include/ykgpu.h (host only).  Returns (spheres ctypes array, Camera)."""
+    lib = load_library()
+    n, cam = ctypes.c_uint32(0), Camera()
+    _check(lib.yk_scene_build(name.encode(), seed, None, 0, ctypes.byref(n), ctypes.byref(cam)))
+    arr = (Sphere * n.value)()
+    _check(lib.yk_scene_build(name.encode(), seed, arr, n.value, ctypes.byref(n), None))
+    return arr, cam
+
+
+class Renderer:
+    """One device context (ykgpu_context): owns the scene in HBM, scratch and a stream."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        self._ctx = ctypes.c_void_p()
+        _check(self._lib.ykgpu_context_create(device, ctypes.byref(self._ctx)))
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            self._lib.ykgpu_context_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_scene(self, spheres, camera: Camera):
+        arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
+        _check(self._lib.ykgpu_set_scene(self._ctx, arr, len(arr), ctypes.byref(camera)))
+
+    def render(self, params: RenderParams) -> np.ndarray:
+        """Host RGB8 image of the tile: uint8[row_count, W, 3] (image_t layout)."""
+        out = np.empty((params.row_count, params.image_width, 3), np.uint8)
+        _check(self._lib.ykgpu_render(self._ctx, ctypes.byref(params), out.ctypes.data))
+        return out
+
+    def render_sums(self, params: RenderParams) -> np.ndarray:
+        out = np.empty((params.row_count, params.image_width, 3), np.float64)
+        _check(self._lib.ykgpu_render_sums(self._ctx, ctypes.byref(params), out.ctypes.data))
+        return out
+
+    def render_async(self, params: RenderParams, rgb_device_ptr: int, stream_ptr: int = 0):
+        """Enqueue into device memory (e.g. a torch.uint8 CUDA tensor's data_ptr())."""
+        _check(self._lib.ykgpu_render_async(self._ctx, ctypes.byref(params),
+                                            ctypes.c_void_p(rgb_device_ptr),
+                                            ctypes.c_void_p(stream_ptr or None)))
+
+    def stats(self) -> dict:
+        st = RenderStats()
+        _check(self._lib.ykgpu_get_stats(self._ctx, ctypes.byref(st)))
+        return st.as_dict()
+
+
+__all__ = ["Renderer", "YkError", "build_scene", "reference_camera", "device_count",
+           "make_params", "load_library", "records", "EXPORTS", "LIB_PATH", "CLI_PATH"]

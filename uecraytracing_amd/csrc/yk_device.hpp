@@ -1,0 +1,166 @@
+// yk_device.hpp — per-lane arithmetic of one sample, gfx950 device code.
+//
+// Every function reproduces the reference's IEEE-double evaluation order operation for
+// operation (the file is compiled with -ffp-contract=off: no FMA contraction), so a sample's
+// colour is bit-identical to yk::raytracer<double,double>::ray_color.  Citations are
+// /root/reference/<file>:<line>.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ykd {
+
+// ------------------------------------------------------------------------------------------
+// vec3 (yk/vec3.hpp) — only the operations the hot path uses, same association order.
+struct v3 {
+  double x, y, z;
+};
+__device__ __forceinline__ v3 add(v3 a, v3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ v3 sub(v3 a, v3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ v3 mul(v3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ v3 divs(v3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ v3 neg(v3 a) { return {-a.x, -a.y, -a.z}; }
+// dot(): vec3.hpp:145-147 → (x*x' + y*y') + z*z'
+__device__ __forceinline__ double dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// length_squared(): vec3.hpp:129
+__device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+
+// math::sqrt (math.hpp:10-19): Newton from s/2 until two iterates are equal.  Not IEEE sqrt
+// (differs by an ulp on ~25% of inputs), so it is replayed exactly.  The iteration bound only
+// matters for NaN/inf inputs (finite inputs converge in < 1100 steps; scene values in 5-17).
+__device__ __forceinline__ double nsqrt(double s) {
+  double x = s / 2.0, prev = 0.0;
+  for (int guard = 0; x != prev && guard < 4096; ++guard) {
+    prev = x;
+    x = (x + s / x) / 2.0;
+  }
+  return x;
+}
+
+__device__ __forceinline__ v3 normalized(v3 a) { return divs(a, nsqrt(len2(a))); }  // :127,132
+// reflect(): vec3.hpp:199-202, v - (2*dot(v,n))*n
+__device__ __forceinline__ v3 reflect(v3 v, v3 n) { return sub(v, mul(n, 2.0 * dot(v, n))); }
+// near_zero(): vec3.hpp:76-80 — tests |x|, |y| and |x| again (z is never tested)
+__device__ __forceinline__ bool near_zero(v3 a) {
+  const double ax = a.x > 0 ? a.x : -a.x, ay = a.y > 0 ? a.y : -a.y;
+  return (ax < 1e-8) && (ay < 1e-8) && (ax < 1e-8);
+}
+
+// ------------------------------------------------------------------------------------------
+// mt19937 (random.hpp:43-151), one fresh engine per sample (source.cpp:154-158).
+//
+// A full engine is 624 words; seeding it and twisting it costs ~8 µs per sample on the CPU
+// (90% of the reference's time).  A sample draws 11 words on average (p99 58), so the lane
+// keeps three CURSORS into the seeding sequence x_i instead of the state:
+//   output j (j < 227) = temper( x_{j+397} ^ mix(x_j, x_{j+1}) )      (M_gen_rand, :118-121)
+// with x_i = 1812433253*(x_{i-1} ^ x_{i-1}>>30) + i (seed(), :69-81).  Cursor A carries
+// (x_j, x_{j+1}), cursor B carries x_{j+397}; each draw steps both by one.  Start-up is the
+// 397-step walk of B.  Draw 227 and later need words the first twist already rewrote, so
+// the lane then materialises the real 624-word state in its slot of a global scratch buffer
+// (same seed, same twist) and continues from index 227 — exact for any number of draws.
+constexpr uint32_t kMtN = 624, kMtM = 397, kLazyDraws = kMtN - kMtM;  // 227
+
+__device__ __forceinline__ uint32_t mt_seed_step(uint32_t prev, uint32_t i) {
+  return 1812433253u * (prev ^ (prev >> 30)) + i;
+}
+__device__ __forceinline__ uint32_t mt_mix(uint32_t hi_src, uint32_t lo_src) {
+  const uint32_t y = (hi_src & 0x80000000u) | (lo_src & 0x7fffffffu);
+  return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t z) {  // random.hpp:98-102
+  z ^= (z >> 11);
+  z ^= (z << 7) & 0x9d2c5680u;
+  z ^= (z << 15) & 0xefc60000u;
+  z ^= (z >> 18);
+  return z;
+}
+
+struct MtLane {
+  uint32_t a0, a1, b;  // x_j, x_{j+1}, x_{j+397}
+  uint32_t j;          // index of the next output
+  uint32_t seed;
+  uint32_t* state;     // this lane's 624-word scratch (used only once j reaches 227)
+};
+// A sample used the scratch engine iff it drew more than 227 words.
+__device__ __forceinline__ bool mt_used_fallback(const MtLane& g) { return g.j > kLazyDraws; }
+
+__device__ __forceinline__ void mt_start(MtLane& g, uint32_t seed) {
+  g.seed = seed;
+  g.j = 0;
+  g.a0 = seed;
+  uint32_t x = mt_seed_step(seed, 1);
+  g.a1 = x;
+#pragma unroll 8
+  for (uint32_t i = 2; i <= kMtM; ++i) x = mt_seed_step(x, i);
+  g.b = x;
+}
+
+// The rare path: the real engine in global scratch (seed :69-81, M_gen_rand :114-131).
+// Out of line and by value so the hot path keeps the lane's cursors in registers.
+__device__ __noinline__ uint32_t mt_slow(uint32_t* st, uint32_t seed, uint32_t j) {
+  const uint32_t idx = j % kMtN;
+  if (j == kLazyDraws) {
+    uint32_t x = seed;
+    st[0] = x;
+    for (uint32_t i = 1; i < kMtN; ++i) {
+      x = mt_seed_step(x, i);
+      st[i] = x;
+    }
+  }
+  if (j == kLazyDraws || idx == 0) {
+    uint32_t k = 0;
+    for (; k < kMtN - kMtM; ++k) st[k] = st[k + kMtM] ^ mt_mix(st[k], st[k + 1]);
+    for (; k < kMtN - 1; ++k) st[k] = st[k + kMtM - kMtN] ^ mt_mix(st[k], st[k + 1]);
+    st[kMtN - 1] = st[kMtM - 1] ^ mt_mix(st[kMtN - 1], st[0]);
+  }
+  return st[idx];
+}
+
+__device__ __forceinline__ uint32_t mt_next(MtLane& g) {
+  uint32_t z;
+  if (g.j < kLazyDraws) {
+    z = g.b ^ mt_mix(g.a0, g.a1);
+    g.a0 = g.a1;
+    g.a1 = mt_seed_step(g.a1, g.j + 2);
+    g.b = mt_seed_step(g.b, g.j + kMtM + 1);
+  } else {
+    z = mt_slow(g.state, g.seed, g.j);
+  }
+  ++g.j;
+  return mt_temper(z);
+}
+
+// generate_canonical<double,53> (random.hpp:161-183): two draws, sum = u0 + u1*2^32 rounded
+// once, divided by 2^64 (exact), clamped to 1 - eps/2.
+__device__ __forceinline__ double canonical(MtLane& g) {
+  const double u0 = (double)mt_next(g);
+  const double u1 = (double)mt_next(g);
+  double sum = u0;
+  sum = sum + u1 * 4294967296.0;
+  double r = sum / 18446744073709551616.0;
+  if (r >= 1.0) r = 1.0 - 0x1p-53;
+  return r;
+}
+// uniform_real_distribution::operator() (random.hpp:273-278): c*(b-a)+a
+__device__ __forceinline__ double uniform(MtLane& g, double a, double b) {
+  return (canonical(g) * (b - a)) + a;
+}
+// vec3::random(gen, -1, 1) (vec3.hpp:134-142): x, then y, then z
+__device__ __forceinline__ v3 random_vec(MtLane& g, double lo, double hi) {
+  v3 r;
+  r.x = uniform(g, lo, hi);
+  r.y = uniform(g, lo, hi);
+  r.z = uniform(g, lo, hi);
+  return r;
+}
+
+// Schlick reflectance (dielectric extension; no reference code)
+__device__ __forceinline__ double reflectance(double cosine, double ref_idx) {
+  double r0 = (1 - ref_idx) / (1 + ref_idx);
+  r0 = r0 * r0;
+  const double x = 1 - cosine;
+  return r0 + (1 - r0) * ((((x * x) * x) * x) * x);
+}
+
+}  // namespace ykd

@@ -1,0 +1,581 @@
+// ykgpu_render.hip — the per-pixel sampling loop of UECRayTracing on gfx950 (MI355X), and the
+// C-ABI (include/ykgpu.h) around it.
+//
+// Replaces /root/reference/source.cpp:122-172 (for_each over (row,col) → transform_reduce over
+// samples → to_color3b) and the recursion of yk/raytracer.hpp:19-37.
+//
+// Execution model:
+//   * one PERSISTENT grid sized to the occupancy of the chip; every lane owns one PIXEL at a
+//     time and runs that pixel's samples in order s = 0, 1, ..., spp-1, adding each sample's
+//     colour to a per-lane float64 accumulator.  The reference's sum is strictly sequential
+//     (transform_reduce over an input-iterator iota; see oracle/yk_oracle.c pixel_sum), so
+//     keeping a pixel on one lane is what makes the sum bit-identical without storing samples.
+//   * the recursion is flattened into a loop of SEGMENTS (one closest-hit + scatter each).  A
+//     lane whose path ends starts its next sample on the next trip round the loop, and a lane
+//     whose pixel is done fetches the next pixel from a global counter (one wave-aggregated
+//     atomic per refill, __ballot/__popcll) — active-lane compaction by refill: no lane idles
+//     while the image has pixels left, however long its neighbours' bounce chains are.
+//   * the colour of a path is attenuation_1 * (attenuation_2 * (... * L)) — the reference
+//     multiplies back to front as the recursion unwinds, and double multiplication does not
+//     associate, so the lane keeps the ids of the scattering spheres on a small stack (8 in
+//     registers, the rest in a per-lane global spill) and multiplies back to front at the end.
+//   * sphere geometry is read wave-uniformly (scalar loads through the constant cache); the
+//     world tuple order is the array order, so the closest-hit scan is the reference's.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ykgpu.h"
+#include "yk_device.hpp"
+
+using ykd::v3;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define YK_HIP(call)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(e_ == hipErrorOutOfMemory ? YK_ERR_NOMEM : YK_ERR_DEVICE,               \
+                  std::string(#call) + ": " + hipGetErrorString(e_));                     \
+  } while (0)
+
+// Geometry of one sphere, as the closest-hit scan reads it (32 B: one scalar x8 load).
+// rr = radius*radius computed on the host with the same IEEE multiply as sphere.hpp:33.
+struct alignas(32) SphereGeo {
+  double cx, cy, cz, rr;
+};
+// Shading data, read once per segment by the lane that hit the sphere.
+struct alignas(16) SphereMat {
+  double ar, ag, ab, fuzz;
+  double radius, ior;
+  uint32_t kind, pad0;
+  uint64_t pad1;
+};
+static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
+
+constexpr int kBlock = 256;
+constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
+
+struct KernelArgs {
+  yk_camera cam;
+  uint32_t W, H, spp, max_depth;
+  uint32_t seed0, row_begin, row_count, row_stride;
+  uint32_t nspheres, npix, flags, id_stride;
+  double t_min;
+  const SphereGeo* __restrict__ geo;
+  const SphereMat* __restrict__ mat;
+  uint8_t* rgb;
+  double* sums;
+  uint32_t* pixel_counter;
+  uint32_t* mt_scratch;
+  uint16_t* id_scratch;
+  unsigned long long* counters;  // [segments, sphere_tests, sqrt_calls, mt_fallbacks]
+};
+
+__device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
+
+__global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+
+  ykd::MtLane g;
+  g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
+  g.a0 = g.a1 = g.b = g.j = g.seed = 0;
+  uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
+
+  const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
+  const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
+  const v3 lens_u = ld3(ka.cam.lens_u), lens_v = ld3(ka.cam.lens_v);
+  const double lens_r = ka.cam.lens_radius;
+
+  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0;
+
+  uint32_t pix = 0, s = 0, depth = 0, nstk = 0;
+  uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // newest attenuation id in st0's low half
+  double acc_r = 0, acc_g = 0, acc_b = 0;
+  v3 o = {0, 0, 0}, d = {0, 0, 0};
+  bool have_pixel = false, in_path = false;
+
+  for (;;) {
+    // ---- refill: lanes without a pixel take the next ones, one atomic per wave ----------
+    if (!have_pixel) {
+      const unsigned long long m = __ballot(1);
+      const int leader = __ffsll((long long)m) - 1;
+      uint32_t base = 0;
+      if ((int)lane == leader) base = atomicAdd(ka.pixel_counter, (uint32_t)__popcll(m));
+      base = __shfl(base, leader);
+      const uint32_t mine = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (mine >= ka.npix) break;
+      pix = mine;
+      s = 0;
+      acc_r = acc_g = acc_b = 0.0;
+      have_pixel = true;
+      in_path = false;
+    }
+
+    // ---- start sample s of the pixel: seed, jitter, camera ray (source.cpp:154-165) ------
+    if (!in_path) {
+      const uint32_t tr = pix / ka.W, x = pix - tr * ka.W;
+      const uint32_t y = ka.row_begin + tr * ka.row_stride;
+      ykd::mt_start(g, ka.seed0 + (y * ka.W + x) * ka.spp + s);  // uint32 wrap, :154-158
+      const double u = ((double)x + ykd::uniform(g, 0, 1)) / (double)ka.W;
+      const double v = ((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1)) / (double)ka.H;
+      // camera::get_ray (camera.hpp:29-32): llc + u*horizontal + v*vertical (- origin)
+      d = ykd::sub(ykd::add(ykd::add(cam_llc, ykd::mul(cam_h, u)), ykd::mul(cam_v, v)), cam_o);
+      o = cam_o;
+      if (lens_r > 0) {  // thin-lens extension: random_in_unit_disk by rejection
+        double px, py;
+        do {
+          px = ykd::uniform(g, -1, 1);
+          py = ykd::uniform(g, -1, 1);
+        } while (!(px * px + py * py < 1.0));
+        const double rx = px * lens_r, ry = py * lens_r;
+        const v3 off = ykd::add(ykd::mul(lens_u, rx), ykd::mul(lens_v, ry));
+        o = ykd::add(o, off);
+        d = ykd::sub(d, off);
+      }
+      depth = ka.max_depth;
+      nstk = 0;
+      in_path = true;
+    }
+
+    // ---- one segment of ray_color (raytracer.hpp:19-37) ----------------------------------
+    bool ended = false;
+    double L_r = 0, L_g = 0, L_b = 0;
+    if (depth == 0) {
+      ended = true;  // :23 black
+    } else {
+      ++n_seg;
+      // hittable_list::hit_impl (hittable_list.hpp:32-58) over sphere::hit_impl
+      // (sphere.hpp:25-48): tuple order, t_max shrinks to the last accepted root, so the
+      // closest hit wins and an exact tie goes to the later sphere.
+      const double a = ykd::len2(d);
+      double T = INFINITY;
+      int hid = -1;
+      for (uint32_t i = 0; i < ka.nspheres; ++i) {
+        const SphereGeo sg = ka.geo[i];
+        ++n_test;
+        const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
+        const double hb = ykd::dot(oc, d);
+        const double c = ykd::len2(oc) - sg.rr;
+        const double disc = hb * hb - a * c;
+        if (disc < 0) continue;
+        ++n_sqrt;
+        const double sq = ykd::nsqrt(disc);
+        double root = (-hb - sq) / a;
+        if (root < ka.t_min || T < root) {
+          root = (-hb + sq) / a;
+          if (root < ka.t_min || T < root) continue;
+        }
+        T = root;
+        hid = (int)i;
+      }
+
+      if (hid < 0) {
+        // sky (raytracer.hpp:35-36): t = (normalized(dir).y + 1)/2, lerp white → (.5,.7,1)
+        const double t = (d.y / ykd::nsqrt(ykd::len2(d)) + 1.0) / 2;
+        L_r = (1.0 - t) * 1.0 + t * 0.5;
+        L_g = (1.0 - t) * 1.0 + t * 0.7;
+        L_b = (1.0 - t) * 1.0 + t * 1.0;
+        ended = true;
+      } else {
+        const SphereGeo sg = ka.geo[hid];
+        const SphereMat m = ka.mat[hid];
+        // hit record (sphere.hpp:41-45, hittable.hpp:23-27)
+        const v3 p = ykd::add(o, ykd::mul(d, T));
+        const v3 outward = ykd::divs(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
+        const bool front = ykd::dot(d, outward) < 0;
+        const v3 nrm = front ? outward : ykd::neg(outward);
+        bool scattered = true, push = true;
+        v3 nd;
+        if (m.kind == YK_MATERIAL_LAMBERTIAN) {  // material.hpp:50-59
+          v3 ru = ykd::random_vec(g, -1, 1);
+          ru = ykd::divs(ru, ykd::nsqrt(ykd::len2(ru)));
+          nd = ykd::add(nrm, ru);
+          if (ykd::near_zero(nd)) nd = nrm;
+        } else if (m.kind == YK_MATERIAL_METAL) {  // material.hpp:67-75 (+ fuzz extension)
+          nd = ykd::reflect(ykd::normalized(d), nrm);
+          if (m.fuzz > 0) {  // random_in_unit_sphere, material.hpp:27-30
+            v3 ru = ykd::random_vec(g, -1, 1);
+            ru = ykd::divs(ru, ykd::nsqrt(ykd::len2(ru)));
+            const double k = ykd::uniform(g, 0.01, 0.99);
+            nd = ykd::add(nd, ykd::mul(ykd::mul(ru, k), m.fuzz));
+          }
+          scattered = ykd::dot(nd, nrm) > 0;
+        } else {  // dielectric extension (attenuation (1,1,1): multiplying by 1.0 is exact)
+          push = false;
+          const double ratio = front ? (1.0 / m.ior) : m.ior;
+          const v3 unit = ykd::normalized(d);
+          double ct = ykd::dot(ykd::neg(unit), nrm);
+          if (!(ct < 1.0)) ct = 1.0;
+          const double sn = ykd::nsqrt(1.0 - ct * ct);
+          const bool cannot = ratio * sn > 1.0;
+          if (cannot || ykd::reflectance(ct, ratio) > ykd::uniform(g, 0, 1)) {
+            nd = ykd::reflect(unit, nrm);
+          } else {
+            const v3 perp = ykd::mul(ykd::add(unit, ykd::mul(nrm, ct)), ratio);
+            const double pl = 1.0 - ykd::len2(perp);
+            nd = ykd::add(perp, ykd::mul(nrm, -ykd::nsqrt(pl < 0 ? -pl : pl)));
+          }
+        }
+        if (!scattered) {
+          ended = true;  // absorbed: black (raytracer.hpp:30)
+        } else {
+          if (push) {
+            if (nstk >= kStackRegs) id_spill[nstk - kStackRegs] = (uint16_t)(st3 >> 16);
+            st3 = (st3 << 16) | (st2 >> 16);
+            st2 = (st2 << 16) | (st1 >> 16);
+            st1 = (st1 << 16) | (st0 >> 16);
+            st0 = (st0 << 16) | (uint32_t)hid;
+            ++nstk;
+          }
+          o = p;
+          d = nd;
+          --depth;
+        }
+      }
+    }
+
+    if (ended) {
+      // unwind: attenuation_k * (...) from the deepest scatter outwards (raytracer.hpp:31)
+      while (nstk > 0) {
+        const uint32_t id = st0 & 0xffffu;
+        st0 = (st0 >> 16) | (st1 << 16);
+        st1 = (st1 >> 16) | (st2 << 16);
+        st2 = (st2 >> 16) | (st3 << 16);
+        st3 = (st3 >> 16) | (nstk > kStackRegs ? ((uint32_t)id_spill[nstk - kStackRegs - 1] << 16) : 0u);
+        --nstk;
+        const SphereMat m = ka.mat[id];
+        L_r = m.ar * L_r;
+        L_g = m.ag * L_g;
+        L_b = m.ab * L_b;
+      }
+      if (ykd::mt_used_fallback(g)) ++n_fb;
+      acc_r = acc_r + L_r;  // transform_reduce, strictly in sample order
+      acc_g = acc_g + L_g;
+      acc_b = acc_b + L_b;
+      in_path = false;
+      if (++s == ka.spp) {
+        // to_color3b (source.cpp:73-83): /spp, math::sqrt, clamp [0, .999], *256, truncate
+        const size_t o3 = (size_t)pix * 3;
+        const double spp = (double)ka.spp;
+        double q[3] = {acc_r, acc_g, acc_b};
+        if (ka.sums) {
+          ka.sums[o3 + 0] = acc_r;
+          ka.sums[o3 + 1] = acc_g;
+          ka.sums[o3 + 2] = acc_b;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          double vq = ykd::nsqrt(q[c] / spp);
+          vq = (vq < 0.0) ? 0.0 : (0.999 < vq) ? 0.999 : vq;
+          ka.rgb[o3 + c] = (uint8_t)(uint32_t)(vq * 256);
+        }
+        have_pixel = false;
+      }
+    }
+  }
+
+  if (ka.flags & YK_FLAG_COUNT_WORK) {
+    atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
+    atomicAdd(&ka.counters[1], (unsigned long long)n_test);
+    atomicAdd(&ka.counters[2], (unsigned long long)n_sqrt);
+  }
+  if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
+}
+
+}  // namespace
+
+// =========================================================================================
+// C-ABI
+// =========================================================================================
+struct ykgpu_context {
+  int device = 0;
+  int cus = 0;
+  int grid = 0;  // persistent blocks
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  SphereGeo* d_geo = nullptr;
+  SphereMat* d_mat = nullptr;
+  uint32_t nspheres = 0;
+  yk_camera cam{};
+  bool have_scene = false;
+  uint32_t* d_counter = nullptr;        // [0] pixel counter
+  unsigned long long* d_stats = nullptr;  // 4 counters
+  uint32_t* d_mt = nullptr;             // grid*256*624 words
+  uint16_t* d_ids = nullptr;            // grid*256*id_stride
+  uint32_t id_stride = 0;
+  uint8_t* d_rgb = nullptr;
+  size_t rgb_cap = 0;
+  double* d_sums = nullptr;
+  size_t sums_cap = 0;
+  yk_render_stats stats{};
+  bool stats_pending = false;
+  std::chrono::steady_clock::time_point t0;
+};
+
+namespace {
+
+int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
+  if (!ctx || !p) return fail(YK_ERR_INVALID, "null context or params");
+  if (!ctx->have_scene) return fail(YK_ERR_NO_SCENE, "ykgpu_set_scene was not called");
+  if (!p->image_width || !p->image_height || !p->samples_per_pixel)
+    return fail(YK_ERR_INVALID, "image_width, image_height and samples_per_pixel must be > 0");
+  if (!p->row_count) return fail(YK_ERR_INVALID, "row_count must be > 0");
+  if (!p->row_stride) return fail(YK_ERR_INVALID, "row_stride must be > 0");
+  if ((uint64_t)p->row_begin + (uint64_t)(p->row_count - 1) * p->row_stride >= p->image_height)
+    return fail(YK_ERR_INVALID, "row range outside the image");
+  if ((uint64_t)p->row_count * p->image_width >= (1ull << 31))
+    return fail(YK_ERR_INVALID, "tile larger than 2^31 pixels");
+  if (p->precision != YK_PRECISION_FP64) return fail(YK_ERR_UNSUPPORTED, "precision mode");
+  if (p->rng != YK_RNG_MT19937) return fail(YK_ERR_UNSUPPORTED, "rng mode");
+  if (!(p->t_min >= 0)) return fail(YK_ERR_INVALID, "t_min must be >= 0");
+  return YK_OK;
+}
+
+int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
+  const size_t lanes = (size_t)ctx->grid * kBlock;
+  if (!ctx->d_mt) YK_HIP(hipMalloc(&ctx->d_mt, lanes * ykd::kMtN * sizeof(uint32_t)));
+  const uint32_t need = max_depth > kStackRegs ? max_depth : 1;
+  if (need > ctx->id_stride) {
+    if (ctx->d_ids) YK_HIP(hipFree(ctx->d_ids));
+    ctx->d_ids = nullptr;
+    YK_HIP(hipMalloc(&ctx->d_ids, lanes * need * sizeof(uint16_t)));
+    ctx->id_stride = need;
+  }
+  return YK_OK;
+}
+
+int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
+           hipStream_t st) {
+  int rc = ensure_scratch(ctx, p->max_depth);
+  if (rc) return rc;
+  KernelArgs ka;
+  ka.cam = ctx->cam;
+  ka.W = p->image_width;
+  ka.H = p->image_height;
+  ka.spp = p->samples_per_pixel;
+  ka.max_depth = p->max_depth;
+  ka.seed0 = p->seed0;
+  ka.row_begin = p->row_begin;
+  ka.row_count = p->row_count;
+  ka.row_stride = p->row_stride;
+  ka.nspheres = ctx->nspheres;
+  ka.npix = p->row_count * p->image_width;
+  ka.flags = p->flags;
+  ka.id_stride = ctx->id_stride;
+  ka.t_min = p->t_min;
+  ka.geo = ctx->d_geo;
+  ka.mat = ctx->d_mat;
+  ka.rgb = rgb_dev;
+  ka.sums = sums_dev;
+  ka.pixel_counter = ctx->d_counter;
+  ka.mt_scratch = ctx->d_mt;
+  ka.id_scratch = ctx->d_ids;
+  ka.counters = ctx->d_stats;
+  YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
+  YK_HIP(hipMemsetAsync(ctx->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  YK_HIP(hipEventRecord(ctx->ev0, st));
+  hipLaunchKernelGGL(yk_render_persistent, dim3(ctx->grid), dim3(kBlock), 0, st, ka);
+  YK_HIP(hipGetLastError());
+  YK_HIP(hipEventRecord(ctx->ev1, st));
+  ctx->stats = yk_render_stats{};
+  ctx->stats.samples = (uint64_t)ka.npix * ka.spp;
+  ctx->stats.launches = 1;
+  ctx->stats.grid_blocks = (uint32_t)ctx->grid;
+  ctx->stats_pending = true;
+  return YK_OK;
+}
+
+int finish_stats(ykgpu_context* ctx) {
+  if (!ctx->stats_pending) return YK_OK;
+  YK_HIP(hipEventSynchronize(ctx->ev1));
+  float ms = 0;
+  YK_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  unsigned long long c[4];
+  YK_HIP(hipMemcpy(c, ctx->d_stats, sizeof(c), hipMemcpyDeviceToHost));
+  ctx->stats.kernel_ms = ms;
+  ctx->stats.segments = c[0];
+  ctx->stats.sphere_tests = c[1];
+  ctx->stats.sqrt_calls = c[2];
+  ctx->stats.mt_fallbacks = c[3];
+  ctx->stats_pending = false;
+  return YK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t ykgpu_abi_version(void) { return YKGPU_ABI_VERSION; }
+
+const char* ykgpu_last_error(void) { return g_last_error.c_str(); }
+
+int ykgpu_device_count(int* count) {
+  if (!count) return fail(YK_ERR_INVALID, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(YK_ERR_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = n;
+  return YK_OK;
+}
+
+int ykgpu_context_create(int device, ykgpu_context** out) {
+  if (!out) return fail(YK_ERR_INVALID, "null out");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return fail(YK_ERR_DEVICE, "no HIP device (the renderer has no CPU fallback)");
+  if (device < 0 || device >= n) return fail(YK_ERR_INVALID, "device index out of range");
+  YK_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  YK_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(YK_ERR_DEVICE, std::string("built for gfx950, device is ") + prop.gcnArchName);
+  auto* ctx = new ykgpu_context();
+  ctx->device = device;
+  ctx->cus = prop.multiProcessorCount;
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent, kBlock, 0);
+  if (e != hipSuccess || per_cu < 1) per_cu = 1;
+  ctx->grid = per_cu * ctx->cus;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+      hipMalloc(&ctx->d_counter, 16) != hipSuccess ||
+      hipMalloc(&ctx->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess) {
+    ykgpu_context_destroy(ctx);
+    return fail(YK_ERR_DEVICE, "context resources");
+  }
+  *out = ctx;
+  return YK_OK;
+}
+
+int ykgpu_context_destroy(ykgpu_context* ctx) {
+  if (!ctx) return YK_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(ctx->d_geo);
+  (void)hipFree(ctx->d_mat);
+  (void)hipFree(ctx->d_counter);
+  (void)hipFree(ctx->d_stats);
+  (void)hipFree(ctx->d_mt);
+  (void)hipFree(ctx->d_ids);
+  (void)hipFree(ctx->d_rgb);
+  (void)hipFree(ctx->d_sums);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return YK_OK;
+}
+
+int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count,
+                    const yk_camera* camera) {
+  if (!ctx || !spheres || !camera) return fail(YK_ERR_INVALID, "null argument");
+  if (count == 0 || count > 65535) return fail(YK_ERR_INVALID, "sphere count must be 1..65535");
+  std::vector<SphereGeo> geo(count);
+  std::vector<SphereMat> mat(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    const yk_sphere& s = spheres[i];
+    if (s.material > YK_MATERIAL_DIELECTRIC) return fail(YK_ERR_INVALID, "unknown material kind");
+    geo[i] = {s.center[0], s.center[1], s.center[2], s.radius * s.radius};
+    mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0u, 0ull};
+  }
+  YK_HIP(hipSetDevice(ctx->device));
+  YK_HIP(hipStreamSynchronize(ctx->stream));
+  if (count > ctx->nspheres || !ctx->d_geo) {
+    (void)hipFree(ctx->d_geo);
+    (void)hipFree(ctx->d_mat);
+    ctx->d_geo = nullptr;
+    ctx->d_mat = nullptr;
+    YK_HIP(hipMalloc(&ctx->d_geo, count * sizeof(SphereGeo)));
+    YK_HIP(hipMalloc(&ctx->d_mat, count * sizeof(SphereMat)));
+  }
+  YK_HIP(hipMemcpy(ctx->d_geo, geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
+  YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));
+  ctx->nspheres = count;
+  ctx->cam = *camera;
+  ctx->have_scene = true;
+  return YK_OK;
+}
+
+int ykgpu_render_async(ykgpu_context* ctx, const yk_render_params* p, void* rgb_device,
+                       void* stream) {
+  int rc = check_params(ctx, p);
+  if (rc) return rc;
+  if (!rgb_device) return fail(YK_ERR_INVALID, "null output");
+  YK_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  ctx->t0 = std::chrono::steady_clock::now();
+  return launch(ctx, p, (uint8_t*)rgb_device, nullptr, st);
+}
+
+static int render_host(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_host,
+                       double* sums_host) {
+  int rc = check_params(ctx, p);
+  if (rc) return rc;
+  YK_HIP(hipSetDevice(ctx->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t npix = (size_t)p->row_count * p->image_width;
+  if (npix * 3 > ctx->rgb_cap) {
+    (void)hipFree(ctx->d_rgb);
+    ctx->d_rgb = nullptr;
+    YK_HIP(hipMalloc(&ctx->d_rgb, npix * 3));
+    ctx->rgb_cap = npix * 3;
+  }
+  if (sums_host && npix * 3 > ctx->sums_cap) {
+    (void)hipFree(ctx->d_sums);
+    ctx->d_sums = nullptr;
+    YK_HIP(hipMalloc(&ctx->d_sums, npix * 3 * sizeof(double)));
+    ctx->sums_cap = npix * 3;
+  }
+  rc = launch(ctx, p, ctx->d_rgb, sums_host ? ctx->d_sums : nullptr, ctx->stream);
+  if (rc) return rc;
+  if (rgb_host) YK_HIP(hipMemcpyAsync(rgb_host, ctx->d_rgb, npix * 3, hipMemcpyDeviceToHost, ctx->stream));
+  if (sums_host)
+    YK_HIP(hipMemcpyAsync(sums_host, ctx->d_sums, npix * 3 * sizeof(double), hipMemcpyDeviceToHost,
+                          ctx->stream));
+  YK_HIP(hipStreamSynchronize(ctx->stream));
+  rc = finish_stats(ctx);
+  ctx->stats.total_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
+}
+
+int ykgpu_render(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_host) {
+  if (!rgb_host) return fail(YK_ERR_INVALID, "null output");
+  return render_host(ctx, p, rgb_host, nullptr);
+}
+
+int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* p, double* sums_host) {
+  if (!sums_host) return fail(YK_ERR_INVALID, "null output");
+  return render_host(ctx, p, nullptr, sums_host);
+}
+
+int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out) {
+  if (!ctx || !out) return fail(YK_ERR_INVALID, "null argument");
+  YK_HIP(hipSetDevice(ctx->device));
+  int rc = finish_stats(ctx);
+  if (rc) return rc;
+  *out = ctx->stats;
+  return YK_OK;
+}
+
+}  // extern "C"
