@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark of the per-pixel sampling loop on MI355X (BASELINE.json metric).
+
+One STEP = one full render of the headline configuration (BASELINE config 3): 1920x1080,
+512 spp, max_depth 50, the ~485-sphere RTIOW final scene (seed 42), FP64 / mt19937, bit-exact to
+the reference's arithmetic.  Inputs (scene, camera) are resident in HBM before the timed region;
+the output RGB8 image is produced in HBM (rank 0 holds the assembled image).
+
+N > 1 (one process per GPU, torchrun): the image's rows are dealt cyclically (row r → rank r mod
+N), each rank renders its tile into device memory, and the tiles are gathered to rank 0 over
+RCCL (torch.distributed 'nccl') and de-interleaved on device — all inside the timed region.
+The total image is fixed, so this is STRONG scaling.
+
+Prints ONE JSON line on rank 0.  The `roofline` object is computed from HIP events recorded on
+the render stream around every timed launch and the kernel's own work counters; the
+`cpu_baseline` is the CPU oracle restatement (oracle/yk_oracle.c, "port") on a strided row
+subset of the same workload, on this host's cores, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/sec at 1920x1080x512spp (~500 spheres); per-pixel RMSE vs CPU"
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP32 vector 157.3 TF / 2, MI355X_MICROARCH.md)
+HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+FLOPS_PER_SPHERE_TEST = 17    # sphere.hpp:29-33 discriminant: 3 sub, 6 mul+4 add (dots), 1 sub, 2 mul+1 sub
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--spp", type=int, default=512)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--scene", default="final")
+    ap.add_argument("--scene-seed", type=int, default=42)
+    ap.add_argument("--seed0", type=int, default=404)
+    ap.add_argument("--cpu-row-step", type=int, default=45,
+                    help="CPU baseline renders every k-th row at full spp")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    import torch.distributed as dist
+
+    import uecraytracing_amd as yk
+    from uecraytracing_amd.records import image_height_for, make_params
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    W, spp, depth = args.width, args.spp, args.depth
+    H = image_height_for(W)
+    spheres, cam = yk.build_scene(args.scene, args.scene_seed)
+    rows_mine = len(range(rank, H, world))
+    rows_max = -(-H // world)
+    params = make_params(W, H, spp, depth, args.seed0, rows=(rank, rows_mine, world), flags=1)
+
+    ren = yk.Renderer(local)
+    ren.set_scene(spheres, cam)  # world + camera uploaded to HBM before any timing
+    stream = torch.cuda.Stream(device=dev)
+    tile = torch.zeros((rows_max, W, 3), dtype=torch.uint8, device=dev)
+    gathered = torch.empty((world, rows_max, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+    # row r of the image is row r // world of rank r % world's tile
+    perm = torch.tensor([(r % world) * rows_max + r // world for r in range(H)], device=dev)
+    image = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+    ev = []
+
+    def step(timed):
+        with torch.cuda.stream(stream):
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            ren.render_async(params, tile.data_ptr(), stream.cuda_stream)
+            if timed:
+                e1.record(stream)
+                ev.append((e0, e1))
+            if world > 1:
+                dist.gather(tile, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+                if rank == 0:
+                    torch.index_select(gathered.reshape(world * rows_max, W, 3), 0, perm, out=image)
+            else:
+                image.copy_(tile[:H])
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    st = ren.stats()  # work counters of the last (identical) launch
+    total_samples = W * H * spp
+    value = total_samples * args.steps / elapsed / 1e6
+
+    # roofline of the dominant kernel (this rank's launch)
+    flops = st["sphere_tests"] * FLOPS_PER_SPHERE_TEST
+    achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
+    hbm_bytes = rows_mine * W * 3 + len(spheres) * 96  # RGB8 out + scene in (algorithmic)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        if rec.get("workload") == f"{args.scene}{args.scene_seed}_{W}x{H}x{spp}_d{depth}_n{world}":
+            traffic = rec.get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"BASELINE config 3: {W}x{H}x{spp}spp, max_depth {depth}, RTIOW final "
+                        f"scene ({len(spheres)} spheres, generator seed {args.scene_seed}), "
+                        f"seed0 {args.seed0}, mt19937 + FP64 bit-exact",
+            "image": f"{W}x{H}", "spp": spp, "max_depth": depth, "spheres": len(spheres),
+            "partition": f"cyclic rows over {world} GPU(s), RCCL gather to rank 0",
+        },
+        "roofline": {
+            "bound": "valu",
+            "achieved": round(achieved_tf, 3),
+            "peak": FP64_VALU_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "kernel_ms": round(kernel_ms, 3),
+            "algorithmic": f"{FLOPS_PER_SPHERE_TEST} FP64 flop per ray-sphere discriminant x "
+                           f"{st['sphere_tests']} tests per launch",
+            "hbm": {"achieved_gbps": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 4),
+                    "peak_gbps": HBM_PEAK_GBPS,
+                    "frac": hbm_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
+            "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
+            "tests_per_segment": round(st["sphere_tests"] / max(1, st["segments"]), 2),
+        },
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import numpy as np
+
+        import oracle_lib
+
+        rows = list(range(0, H, args.cpu_row_step))
+        nthreads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        cp = make_params(W, H, spp, depth, args.seed0,
+                         rows=(0, len(rows), args.cpu_row_step))
+        t = time.perf_counter()
+        cpu_rgb, _, _, _ = oracle_lib.render(spheres, cam, cp, nthreads=nthreads)
+        dt = time.perf_counter() - t
+        n = len(rows) * W * spp
+        gpu_rows = image[::args.cpu_row_step].cpu().numpy()
+        diff = (gpu_rows.astype(np.float64) - cpu_rgb.astype(np.float64)) / 255.0
+        result["cpu_baseline"] = {
+            "value": round(n / dt / 1e6, 4),
+            "unit": "Msamples/s",
+            "cores": nthreads,
+            "kind": "port",
+            "sample": f"{len(rows)} rows (every {args.cpu_row_step}th) x {W} px x {spp} spp = "
+                      f"{n} samples of the same workload, {dt:.1f} s, oracle/yk_oracle.c "
+                      f"(-O2, {nthreads} threads)",
+        }
+        result["parity_vs_cpu"] = {
+            "rows_compared": len(rows),
+            "rmse": float(np.sqrt(np.mean(diff ** 2))),
+            "max_abs_levels": int(np.abs(gpu_rows.astype(int) - cpu_rgb.astype(int)).max()),
+            "bytes_differing": int((gpu_rows != cpu_rgb).sum()),
+        }
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ren.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
