@@ -52,7 +52,9 @@ enum { YK_RNG_MT19937 = 0 };
 
 /* yk_render_params.flags */
 enum {
-  YK_FLAG_COUNT_WORK = 1u /* count segments / sphere tests (ykgpu_get_stats) */
+  YK_FLAG_COUNT_WORK = 1u, /* count segments / sphere tests (ykgpu_get_stats)              */
+  YK_FLAG_LINEAR_SCAN = 2u /* closest hit by the reference's linear scan instead of the BVH
+                              (same results; A/B and debugging)                              */
 };
 
 enum {
@@ -112,6 +114,8 @@ typedef struct yk_render_stats {
   uint64_t sphere_tests;   /* ray-sphere discriminant tests (flag COUNT_WORK)          */
   uint64_t sqrt_calls;     /* Newton square roots on hit candidates (flag COUNT_WORK)  */
   uint64_t mt_fallbacks;   /* samples that needed the full 624-word MT state           */
+  uint64_t node_visits;    /* BVH inner nodes visited (flag COUNT_WORK)                */
+  uint64_t linear_scans;   /* segments served by the exact linear scan (flag COUNT_WORK)*/
   uint32_t launches;       /* path-tracing launches in the call                        */
   uint32_t grid_blocks;    /* persistent grid size                                     */
 } yk_render_stats;

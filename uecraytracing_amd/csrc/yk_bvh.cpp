@@ -1,0 +1,158 @@
+// yk_bvh.cpp — binned-SAH BVH builder (host).  See yk_bvh.hpp for the culling contract.
+#include "yk_bvh.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+namespace ykbvh {
+namespace {
+
+struct Box {
+  double lo[3] = {INFINITY, INFINITY, INFINITY};
+  double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], b.lo[k]);
+      hi[k] = std::max(hi[k], b.hi[k]);
+    }
+  }
+  void grow(const double* p) {
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], p[k]);
+      hi[k] = std::max(hi[k], p[k]);
+    }
+  }
+  double area() const {
+    if (!(hi[0] >= lo[0])) return 0;
+    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Builder {
+  const double* c;
+  std::vector<Box> sbox;     // per sphere, grown by delta
+  std::vector<double> cent;  // centroids
+  std::vector<uint32_t> idx;
+  std::vector<Node> nodes;
+  bool median_only = false;
+  uint32_t max_depth = 0;
+
+  Box bounds(uint32_t b, uint32_t e) const {
+    Box r;
+    for (uint32_t i = b; i < e; ++i) r.grow(sbox[idx[i]]);
+    return r;
+  }
+
+  // returns a child code for the subtree over idx[b, e)
+  int32_t rec(uint32_t b, uint32_t e, uint32_t depth) {
+    const uint32_t n = e - b;
+    if (n <= kMaxLeaf) {
+      max_depth = std::max(max_depth, depth);
+      return ~int32_t((b << 4) | n);
+    }
+    Box cb;
+    for (uint32_t i = b; i < e; ++i) cb.grow(&cent[3 * idx[i]]);
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+      if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
+    uint32_t mid = b + n / 2;
+    const double ext = cb.hi[axis] - cb.lo[axis];
+    if (!median_only && ext > 0) {
+      constexpr int kBins = 16;
+      Box bb[kBins];
+      uint32_t cnt[kBins] = {};
+      auto bin_of = [&](uint32_t s) {
+        int q = int((cent[3 * s + axis] - cb.lo[axis]) / ext * kBins);
+        return std::min(std::max(q, 0), kBins - 1);
+      };
+      for (uint32_t i = b; i < e; ++i) {
+        const int q = bin_of(idx[i]);
+        bb[q].grow(sbox[idx[i]]);
+        ++cnt[q];
+      }
+      double best = INFINITY;
+      int best_q = -1;
+      for (int q = 1; q < kBins; ++q) {
+        Box l, r;
+        uint32_t nl = 0, nr = 0;
+        for (int t = 0; t < q; ++t) { l.grow(bb[t]); nl += cnt[t]; }
+        for (int t = q; t < kBins; ++t) { r.grow(bb[t]); nr += cnt[t]; }
+        if (!nl || !nr) continue;
+        const double cost = l.area() * nl + r.area() * nr;
+        if (cost < best) { best = cost; best_q = q; }
+      }
+      if (best_q > 0) {
+        auto it = std::partition(idx.begin() + b, idx.begin() + e,
+                                 [&](uint32_t s) { return bin_of(s) < best_q; });
+        mid = uint32_t(it - idx.begin());
+      }
+    }
+    if (mid == b || mid == e || median_only || ext == 0) {
+      mid = b + n / 2;
+      std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e,
+                       [&](uint32_t x, uint32_t y) { return cent[3 * x + axis] < cent[3 * y + axis]; });
+    }
+    const int32_t me = int32_t(nodes.size());
+    nodes.emplace_back();
+    const int32_t l = rec(b, mid, depth + 1);
+    const int32_t r = rec(mid, e, depth + 1);
+    const Box bl = bounds(b, mid), br = bounds(mid, e);
+    Node& nd = nodes[me];
+    const Box* kids[2] = {&bl, &br};
+    for (int k = 0; k < 2; ++k) {
+      // outward rounding to float: nextafter past the double bound
+      auto dn = [](double v) { float f = (float)v; return (double)f > v ? std::nextafter(f, -INFINITY) : f; };
+      auto up = [](double v) { float f = (float)v; return (double)f < v ? std::nextafter(f, INFINITY) : f; };
+      nd.lo_x[k] = dn(kids[k]->lo[0]);
+      nd.lo_y[k] = dn(kids[k]->lo[1]);
+      nd.lo_z[k] = dn(kids[k]->lo[2]);
+      nd.hi_x[k] = up(kids[k]->hi[0]);
+      nd.hi_y[k] = up(kids[k]->hi[1]);
+      nd.hi_z[k] = up(kids[k]->hi[2]);
+    }
+    nd.child[0] = l;
+    nd.child[1] = r;
+    nd.pad[0] = nd.pad[1] = 0;
+    return me;
+  }
+};
+
+}  // namespace
+
+Built build(const double* centers, const double* radii, uint32_t n, double camera_extent) {
+  Built out;
+  double ext = camera_extent;
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) ext = std::max(ext, std::fabs(centers[3 * i + k]) + std::fabs(radii[i]));
+  // origins of secondary rays lie on sphere surfaces (|o| <= ext); allow 4x headroom
+  out.origin_bound = 4.0 * ext;
+  out.delta = (float)std::ldexp(out.origin_bound, -21);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    Builder bd;
+    bd.c = centers;
+    bd.median_only = attempt == 1;
+    bd.sbox.resize(n);
+    bd.cent.assign(centers, centers + 3 * size_t(n));
+    bd.idx.resize(n);
+    std::iota(bd.idx.begin(), bd.idx.end(), 0u);
+    for (uint32_t i = 0; i < n; ++i) {
+      const double r = std::fabs(radii[i]) + out.delta;
+      for (int k = 0; k < 3; ++k) {
+        bd.sbox[i].lo[k] = centers[3 * i + k] - r;
+        bd.sbox[i].hi[k] = centers[3 * i + k] + r;
+      }
+    }
+    out.root = bd.rec(0, n, 0);
+    out.depth = bd.max_depth;
+    if (out.depth <= kMaxDepth || attempt == 1) {
+      out.nodes = std::move(bd.nodes);
+      out.order = std::move(bd.idx);
+      break;
+    }
+  }
+  return out;
+}
+
+}  // namespace ykbvh

@@ -1,0 +1,44 @@
+// yk_bvh.hpp — bounding volume hierarchy over the world's spheres (host build, device layout).
+//
+// The BVH only CULLS: it never decides a hit.  The closest-hit rule of the reference
+// (hittable_list.hpp:32-58: minimum root, exact ties to the later tuple index) is applied to
+// the surviving candidates with the reference's exact arithmetic, so the result is identical to
+// the ordered linear scan whatever the tree looks like.  Culling is conservative:
+//   * boxes are the spheres' bounds grown by kDelta and rounded outward to float;
+//   * kDelta >= 2^-21 * origin_bound, so a ray origin rounded to float moves by less than the
+//     growth, and every root the exact test can return lies inside the grown box;
+//   * slab distances computed in float are compared with a 2^-20 relative slack.
+// Rays whose origin lies beyond origin_bound use the exact linear scan instead.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace ykbvh {
+
+// Binary node, both children's boxes stored in the parent: 64 bytes, 4 x 16-B loads.
+// child >= 0: inner node index; child < 0: leaf, ~child = first << 4 | count (count 1..15).
+struct alignas(16) Node {
+  float lo_x[2], lo_y[2], lo_z[2];
+  float hi_x[2], hi_y[2], hi_z[2];
+  int32_t child[2];
+  int32_t pad[2];
+};
+static_assert(sizeof(Node) == 64, "Node layout");
+
+struct Built {
+  std::vector<Node> nodes;      // nodes[0] is the root when root >= 0
+  std::vector<uint32_t> order;  // leaf slots → original sphere index (tuple order)
+  int32_t root = 0;             // root code (a leaf code when the scene has one leaf)
+  uint32_t depth = 0;           // longest root-to-leaf path (inner nodes)
+  double origin_bound = 0;      // |o|_inf above which a ray uses the exact linear scan
+  float delta = 0;              // box growth
+};
+
+// centers: 3 doubles per sphere; radii may be negative (hollow shells: |r| is used).
+Built build(const double* centers, const double* radii, uint32_t n, double camera_extent);
+
+constexpr uint32_t kMaxLeaf = 4;
+constexpr uint32_t kMaxDepth = 32;  // traversal stack capacity (device, LDS)
+
+}  // namespace ykbvh

@@ -23,6 +23,7 @@
 //     world tuple order is the array order, so the closest-hit scan is the reference's.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -32,6 +33,7 @@
 #include <vector>
 
 #include "../../include/ykgpu.h"
+#include "yk_bvh.hpp"
 #include "yk_device.hpp"
 
 using ykd::v3;
@@ -68,7 +70,9 @@ struct alignas(16) SphereMat {
 static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 
 constexpr int kBlock = 256;
+constexpr int kCounters = 8;
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
+constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 
 struct KernelArgs {
   yk_camera cam;
@@ -76,6 +80,12 @@ struct KernelArgs {
   uint32_t seed0, row_begin, row_count, row_stride;
   uint32_t nspheres, npix, flags, id_stride;
   double t_min;
+  double origin_bound;  // |o|_inf beyond which the BVH's float culling is not proven sound
+  int32_t bvh_root;
+  uint32_t pad0;
+  const ykbvh::Node* __restrict__ nodes;
+  const SphereGeo* __restrict__ leaf_geo;  // spheres in BVH leaf order
+  const uint32_t* __restrict__ leaf_ids;   // leaf slot → tuple index
   const SphereGeo* __restrict__ geo;
   const SphereMat* __restrict__ mat;
   uint8_t* rgb;
@@ -83,8 +93,80 @@ struct KernelArgs {
   uint32_t* pixel_counter;
   uint32_t* mt_scratch;
   uint16_t* id_scratch;
-  unsigned long long* counters;  // [segments, sphere_tests, sqrt_calls, mt_fallbacks]
+  unsigned long long* counters;  // [segments, sphere_tests, sqrt_calls, mt_fallbacks, nodes]
 };
+
+struct Hit {
+  double T;
+  int hid;
+  uint32_t tests, sqrts;
+};
+
+// The reference's closest-hit scan verbatim (hittable_list.hpp:32-58 over sphere.hpp:25-48):
+// tuple order, t_max shrinking to the last accepted root.  Used for rays the BVH cannot serve
+// (degenerate direction, origin beyond the proven float range, candidate-list overflow) and,
+// with kFlagLinearScan, as the A/B reference of the BVH path.
+__device__ __noinline__ Hit scan_linear(const SphereGeo* __restrict__ geo, uint32_t n, v3 o, v3 d,
+                                        double tmin) {
+  const double a = ykd::len2(d);
+  Hit h{INFINITY, -1, 0, 0};
+  for (uint32_t i = 0; i < n; ++i) {
+    const SphereGeo sg = geo[i];
+    ++h.tests;
+    const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
+    const double hb = ykd::dot(oc, d);
+    const double c = ykd::len2(oc) - sg.rr;
+    const double disc = hb * hb - a * c;
+    if (disc < 0) continue;
+    ++h.sqrts;
+    const double sq = ykd::nsqrt(disc);
+    double root = (-hb - sq) / a;
+    if (root < tmin || h.T < root) {
+      root = (-hb + sq) / a;
+      if (root < tmin || h.T < root) continue;
+    }
+    h.T = root;
+    h.hid = (int)i;
+  }
+  return h;
+}
+
+__device__ __forceinline__ float safe_rcp(float x) {
+  return fabsf(x) > 1e-30f ? 1.0f / x : copysignf(1e30f, x);
+}
+
+// Candidate list entry insertion with static register indexing (no scratch).
+#define YK_CAND_SET(K, ID, LB) \
+  do {                         \
+    if ((K) == 0) { c0 = ID; l0 = LB; }       \
+    else if ((K) == 1) { c1 = ID; l1 = LB; }  \
+    else if ((K) == 2) { c2 = ID; l2 = LB; }  \
+    else { c3 = ID; l3 = LB; }                \
+  } while (0)
+
+// Exact value of sphere i's root under the reference's acceptance rule, ignoring t_max
+// (sphere.hpp:35-39): root1 if root1 >= t_min, else root2 if root2 >= t_min, else none.
+__device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ geo, uint32_t i,
+                                                v3 o, v3 d, double a, double tmin, Hit& best) {
+  const SphereGeo sg = geo[i];
+  const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
+  const double hb = ykd::dot(oc, d);
+  const double c = ykd::len2(oc) - sg.rr;
+  const double disc = hb * hb - a * c;
+  if (disc < 0) return;  // never taken: the candidate passed the same test
+  ++best.sqrts;
+  const double sq = ykd::nsqrt(disc);
+  double r = (-hb - sq) / a;
+  if (r < tmin) {
+    r = (-hb + sq) / a;
+    if (r < tmin) return;
+  }
+  // closest wins; an exact tie goes to the later tuple index (hittable_list.hpp:36-43)
+  if (r < best.T || (r == best.T && (int)i > best.hid)) {
+    best.T = r;
+    best.hid = (int)i;
+  }
+}
 
 __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
 
@@ -102,7 +184,8 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
   const v3 lens_u = ld3(ka.cam.lens_u), lens_v = ld3(ka.cam.lens_v);
   const double lens_r = ka.cam.lens_radius;
 
-  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0;
+  __shared__ int32_t s_stack[ykbvh::kMaxDepth][kBlock];  // per-lane BVH traversal stacks
+  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0;
 
   uint32_t pix = 0, s = 0, depth = 0, nstk = 0;
   uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // newest attenuation id in st0's low half
@@ -164,26 +247,116 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
       // (sphere.hpp:25-48): tuple order, t_max shrinks to the last accepted root, so the
       // closest hit wins and an exact tie goes to the later sphere.
       const double a = ykd::len2(d);
-      double T = INFINITY;
-      int hid = -1;
-      for (uint32_t i = 0; i < ka.nspheres; ++i) {
-        const SphereGeo sg = ka.geo[i];
-        ++n_test;
-        const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
-        const double hb = ykd::dot(oc, d);
-        const double c = ykd::len2(oc) - sg.rr;
-        const double disc = hb * hb - a * c;
-        if (disc < 0) continue;
-        ++n_sqrt;
-        const double sq = ykd::nsqrt(disc);
-        double root = (-hb - sq) / a;
-        if (root < ka.t_min || T < root) {
-          root = (-hb + sq) / a;
-          if (root < ka.t_min || T < root) continue;
+      const double onorm = fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z)));
+      Hit hit{INFINITY, -1, 0, 0};
+      bool linear = (ka.flags & kFlagLinearScan) || !(a > 0 && a < INFINITY) ||
+                    !(onorm <= ka.origin_bound);
+      if (!linear) {
+        // ---- BVH traversal: cull conservatively, keep every sphere whose exact root could
+        //      be the minimum -------------------------------------------------
+        const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+        const float ix = safe_rcp((float)d.x), iy = safe_rcp((float)d.y), iz = safe_rcp((float)d.z);
+        const double ia = 1.0 / a;
+        const float tminf = (float)ka.t_min;
+        double ustar = INFINITY;  // proven upper bound of the minimum exact root
+        float ustar_f = INFINITY;
+        uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        double l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+        bool overflow = false;
+        int32_t node = ka.bvh_root;
+        uint32_t sp = 0;
+        for (;;) {
+          if (node >= 0) {
+            ++n_node;
+            const ykbvh::Node nd = ka.nodes[node];
+            float tn[2], tf[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const float ax = (nd.lo_x[k] - ox) * ix, bx = (nd.hi_x[k] - ox) * ix;
+              const float ay = (nd.lo_y[k] - oy) * iy, by = (nd.hi_y[k] - oy) * iy;
+              const float az = (nd.lo_z[k] - oz) * iz, bz = (nd.hi_z[k] - oz) * iz;
+              const float n0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+              const float f0 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+              tn[k] = n0 - fabsf(n0) * 0x1p-20f;  // relax by the float error bound
+              tf[k] = f0 + fabsf(f0) * 0x1p-20f;
+            }
+            const bool h0 = tn[0] <= tf[0] && tf[0] >= tminf && tn[0] <= ustar_f;
+            const bool h1 = tn[1] <= tf[1] && tf[1] >= tminf && tn[1] <= ustar_f;
+            if (h0 && h1) {
+              const bool first0 = tn[0] <= tn[1];
+              s_stack[sp][threadIdx.x] = first0 ? nd.child[1] : nd.child[0];
+              ++sp;
+              node = first0 ? nd.child[0] : nd.child[1];
+              continue;
+            }
+            if (h0 || h1) {
+              node = h0 ? nd.child[0] : nd.child[1];
+              continue;
+            }
+          } else {
+            const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
+            for (uint32_t k = 0; k < cnt; ++k) {
+              const SphereGeo sg = ka.leaf_geo[first + k];
+              ++n_test;
+              // the reference's discriminant, bit for bit (sphere.hpp:29-34)
+              const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
+              const double hb = ykd::dot(oc, d);
+              const double c = ykd::len2(oc) - sg.rr;
+              const double disc = hb * hb - a * c;
+              if (disc < 0) continue;
+              // bounds of the exact root: |approx - exact| <= m (500x the rounding bound)
+              const double sq = sqrt(disc);
+              const double r1 = (-hb - sq) * ia, r2 = (-hb + sq) * ia;
+              const double m = (fabs(hb) + sq) * ia * 0x1p-40 + 0x1p-1000;
+              if (r2 + m < ka.t_min) continue;  // both roots certainly behind t_min
+              const double lb = fmax(ka.t_min, r1 - m);
+              const double ub = (r1 - m >= ka.t_min) ? r1 + m : ((r2 - m >= ka.t_min) ? r2 + m : INFINITY);
+              if (!(lb <= ustar)) continue;
+              if (ub < ustar) {
+                ustar = ub;
+                ustar_f = (float)ub * (1.0f + 0x1p-20f);
+              }
+              const uint32_t id = ka.leaf_ids[first + k];
+              if (nc == 4) {  // compact: drop entries the new bound has excluded
+                uint32_t m2 = 0;
+                uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
+                double e0 = l0, e1 = l1, e2 = l2, e3 = l3;
+                if (e0 <= ustar) { YK_CAND_SET(m2, d0, e0); ++m2; }
+                if (e1 <= ustar) { YK_CAND_SET(m2, d1, e1); ++m2; }
+                if (e2 <= ustar) { YK_CAND_SET(m2, d2, e2); ++m2; }
+                if (e3 <= ustar) { YK_CAND_SET(m2, d3, e3); ++m2; }
+                nc = m2;
+              }
+              if (nc < 4) {
+                YK_CAND_SET(nc, id, lb);
+                ++nc;
+              } else {
+                overflow = true;
+              }
+            }
+          }
+          if (sp == 0) break;
+          --sp;
+          node = s_stack[sp][threadIdx.x];
         }
-        T = root;
-        hid = (int)i;
+        if (overflow) {
+          linear = true;
+        } else {
+          // exact evaluation of the survivors, all lanes in step
+          if (nc > 0 && l0 <= ustar) exact_candidate(ka.geo, c0, o, d, a, ka.t_min, hit);
+          if (nc > 1 && l1 <= ustar) exact_candidate(ka.geo, c1, o, d, a, ka.t_min, hit);
+          if (nc > 2 && l2 <= ustar) exact_candidate(ka.geo, c2, o, d, a, ka.t_min, hit);
+          if (nc > 3 && l3 <= ustar) exact_candidate(ka.geo, c3, o, d, a, ka.t_min, hit);
+        }
       }
+      if (linear) {
+        hit = scan_linear(ka.geo, ka.nspheres, o, d, ka.t_min);
+        n_test += hit.tests;
+        ++n_lin;
+      }
+      n_sqrt += hit.sqrts;
+      const double T = hit.T;
+      const int hid = hit.hid;
 
       if (hid < 0) {
         // sky (raytracer.hpp:35-36): t = (normalized(dir).y + 1)/2, lerp white → (.5,.7,1)
@@ -294,6 +467,8 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
     atomicAdd(&ka.counters[1], (unsigned long long)n_test);
     atomicAdd(&ka.counters[2], (unsigned long long)n_sqrt);
+    atomicAdd(&ka.counters[4], (unsigned long long)n_node);
+    atomicAdd(&ka.counters[5], (unsigned long long)n_lin);
   }
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
@@ -315,7 +490,13 @@ struct ykgpu_context {
   yk_camera cam{};
   bool have_scene = false;
   uint32_t* d_counter = nullptr;        // [0] pixel counter
-  unsigned long long* d_stats = nullptr;  // 4 counters
+  unsigned long long* d_stats = nullptr;  // kCounters counters
+  ykbvh::Node* d_nodes = nullptr;
+  SphereGeo* d_leaf_geo = nullptr;
+  uint32_t* d_leaf_ids = nullptr;
+  int32_t bvh_root = 0;
+  uint32_t bvh_depth = 0;
+  double origin_bound = 0;
   uint32_t* d_mt = nullptr;             // grid*256*624 words
   uint16_t* d_ids = nullptr;            // grid*256*id_stride
   uint32_t id_stride = 0;
@@ -379,6 +560,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.flags = p->flags;
   ka.id_stride = ctx->id_stride;
   ka.t_min = p->t_min;
+  ka.origin_bound = ctx->origin_bound;
+  ka.bvh_root = ctx->bvh_root;
+  ka.pad0 = 0;
+  ka.nodes = ctx->d_nodes;
+  ka.leaf_geo = ctx->d_leaf_geo;
+  ka.leaf_ids = ctx->d_leaf_ids;
   ka.geo = ctx->d_geo;
   ka.mat = ctx->d_mat;
   ka.rgb = rgb_dev;
@@ -388,7 +575,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.id_scratch = ctx->d_ids;
   ka.counters = ctx->d_stats;
   YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
-  YK_HIP(hipMemsetAsync(ctx->d_stats, 0, 4 * sizeof(unsigned long long), st));
+  YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
   YK_HIP(hipEventRecord(ctx->ev0, st));
   hipLaunchKernelGGL(yk_render_persistent, dim3(ctx->grid), dim3(kBlock), 0, st, ka);
   YK_HIP(hipGetLastError());
@@ -406,8 +593,10 @@ int finish_stats(ykgpu_context* ctx) {
   YK_HIP(hipEventSynchronize(ctx->ev1));
   float ms = 0;
   YK_HIP(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-  unsigned long long c[4];
+  unsigned long long c[kCounters];
   YK_HIP(hipMemcpy(c, ctx->d_stats, sizeof(c), hipMemcpyDeviceToHost));
+  ctx->stats.node_visits = c[4];
+  ctx->stats.linear_scans = c[5];
   ctx->stats.kernel_ms = ms;
   ctx->stats.segments = c[0];
   ctx->stats.sphere_tests = c[1];
@@ -459,7 +648,7 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_counter, 16) != hipSuccess ||
-      hipMalloc(&ctx->d_stats, 4 * sizeof(unsigned long long)) != hipSuccess) {
+      hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
     ykgpu_context_destroy(ctx);
     return fail(YK_ERR_DEVICE, "context resources");
   }
@@ -475,6 +664,9 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_mat);
   (void)hipFree(ctx->d_counter);
   (void)hipFree(ctx->d_stats);
+  (void)hipFree(ctx->d_nodes);
+  (void)hipFree(ctx->d_leaf_geo);
+  (void)hipFree(ctx->d_leaf_ids);
   (void)hipFree(ctx->d_mt);
   (void)hipFree(ctx->d_ids);
   (void)hipFree(ctx->d_rgb);
@@ -509,6 +701,36 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
     YK_HIP(hipMalloc(&ctx->d_mat, count * sizeof(SphereMat)));
   }
   YK_HIP(hipMemcpy(ctx->d_geo, geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
+  // BVH over the spheres (culling only)
+  std::vector<double> centers(3 * size_t(count)), radii(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    for (int k = 0; k < 3; ++k) centers[3 * i + k] = spheres[i].center[k];
+    radii[i] = spheres[i].radius;
+  }
+  double cam_ext = 0;
+  for (int k = 0; k < 3; ++k) cam_ext = std::max(cam_ext, std::fabs(camera->origin[k]));
+  ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext);
+  if (bvh.depth > ykbvh::kMaxDepth) return fail(YK_ERR_INVALID, "BVH deeper than the traversal stack");
+  std::vector<SphereGeo> leaf_geo(count);
+  for (uint32_t i = 0; i < count; ++i) leaf_geo[i] = geo[bvh.order[i]];
+  (void)hipFree(ctx->d_nodes);
+  (void)hipFree(ctx->d_leaf_geo);
+  (void)hipFree(ctx->d_leaf_ids);
+  ctx->d_nodes = nullptr;
+  ctx->d_leaf_geo = nullptr;
+  ctx->d_leaf_ids = nullptr;
+  const size_t nn = std::max<size_t>(1, bvh.nodes.size());
+  YK_HIP(hipMalloc(&ctx->d_nodes, nn * sizeof(ykbvh::Node)));
+  YK_HIP(hipMalloc(&ctx->d_leaf_geo, count * sizeof(SphereGeo)));
+  YK_HIP(hipMalloc(&ctx->d_leaf_ids, count * sizeof(uint32_t)));
+  if (!bvh.nodes.empty())
+    YK_HIP(hipMemcpy(ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(ykbvh::Node),
+                     hipMemcpyHostToDevice));
+  YK_HIP(hipMemcpy(ctx->d_leaf_geo, leaf_geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
+  YK_HIP(hipMemcpy(ctx->d_leaf_ids, bvh.order.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
+  ctx->bvh_root = bvh.root;
+  ctx->bvh_depth = bvh.depth;
+  ctx->origin_bound = bvh.origin_bound;
   YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));
   ctx->nspheres = count;
   ctx->cam = *camera;

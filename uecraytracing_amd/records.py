@@ -15,6 +15,7 @@ MATERIAL_DIELECTRIC = 2
 PRECISION_FP64 = 0
 RNG_MT19937 = 0
 FLAG_COUNT_WORK = 1
+FLAG_LINEAR_SCAN = 2
 
 YK_OK = 0
 ERRORS = {
@@ -90,6 +91,8 @@ class RenderStats(ctypes.Structure):
         ("sphere_tests", ctypes.c_uint64),
         ("sqrt_calls", ctypes.c_uint64),
         ("mt_fallbacks", ctypes.c_uint64),
+        ("node_visits", ctypes.c_uint64),
+        ("linear_scans", ctypes.c_uint64),
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
     ]
