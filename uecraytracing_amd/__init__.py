@@ -19,6 +19,8 @@ from .records import Camera, RenderParams, RenderStats, Sphere, make_params, sph
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libykgpu.so")
+# tools/ablate.py loads timing-only variants through this override; tests never set it
+LIB_PATH = os.environ.get("YKGPU_LIB_OVERRIDE", LIB_PATH)
 CLI_PATH = os.path.join(LIB_DIR, "raytrace")
 
 EXPORTS = (

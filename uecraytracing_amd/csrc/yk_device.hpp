@@ -29,7 +29,16 @@ __device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.
 // math::sqrt (math.hpp:10-19): Newton from s/2 until two iterates are equal.  Not IEEE sqrt
 // (differs by an ulp on ~25% of inputs), so it is replayed exactly.  The iteration bound only
 // matters for NaN/inf inputs (finite inputs converge in < 1100 steps; scene values in 5-17).
+// YK_ABLATE (timing-only builds, tools/ablate.py; results are WRONG by design):
+//   1 = skip the MT warm-up walk, 2 = hardware sqrt instead of math::sqrt
+#ifndef YK_ABLATE
+#define YK_ABLATE 0
+#endif
+
 __device__ __forceinline__ double nsqrt(double s) {
+#if YK_ABLATE & 2
+  return sqrt(s);
+#endif
   double x = s / 2.0, prev = 0.0;
   for (int guard = 0; x != prev && guard < 4096; ++guard) {
     prev = x;
@@ -91,9 +100,36 @@ __device__ __forceinline__ void mt_start(MtLane& g, uint32_t seed) {
   g.a0 = seed;
   uint32_t x = mt_seed_step(seed, 1);
   g.a1 = x;
+#if YK_ABLATE & 1
+  x ^= 0x5bd1e995u;
+#else
 #pragma unroll 8
   for (uint32_t i = 2; i <= kMtM; ++i) x = mt_seed_step(x, i);
+#endif
   g.b = x;
+}
+
+// Start from a precomputed x_397 (yk_mt_warmup kernel): the lane only sets the A cursor.
+__device__ __forceinline__ void mt_start_from(MtLane& g, uint32_t seed, uint32_t x397) {
+  g.seed = seed;
+  g.j = 0;
+  g.a0 = seed;
+  g.a1 = mt_seed_step(seed, 1);
+  g.b = x397;
+}
+
+// x_397 of the seeding sequence (random.hpp:69-81) for four seeds at once (independent chains
+// interleaved for ILP).  Under YK_ABLATE & 1 the walk is skipped (timing-only builds).
+__device__ __forceinline__ void mt_walk397x4(uint32_t (&x)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = mt_seed_step(x[k], 1);
+#if !(YK_ABLATE & 1)
+#pragma unroll 4
+  for (uint32_t i = 2; i <= kMtM; ++i) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = mt_seed_step(x[k], i);
+  }
+#endif
 }
 
 // The rare path: the real engine in global scratch (seed :69-81, M_gen_rand :114-131).

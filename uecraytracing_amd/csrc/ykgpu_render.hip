@@ -79,10 +79,13 @@ struct KernelArgs {
   uint32_t W, H, spp, max_depth;
   uint32_t seed0, row_begin, row_count, row_stride;
   uint32_t nspheres, npix, flags, id_stride;
+  uint32_t pix_base, pad1;          // this launch renders tile pixels [pix_base, pix_base + npix)
+  const uint32_t* __restrict__ warm;  // x_397 per sample of the launch, [(pix - pix_base)*spp + s]
   double t_min;
   double origin_bound;  // |o|_inf beyond which the BVH's float culling is not proven sound
   int32_t bvh_root;
-  uint32_t pad0;
+  uint32_t n_nodes;
+  uint32_t lds_geo_off, lds_ids_off, lds_stack_off, stack_depth;
   const ykbvh::Node* __restrict__ nodes;
   const SphereGeo* __restrict__ leaf_geo;  // spheres in BVH leaf order
   const uint32_t* __restrict__ leaf_ids;   // leaf slot → tuple index
@@ -170,21 +173,67 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
 
 __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
 
+// Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread,
+// one 16-B store.  out[i] = x_397(seed(i)), i = (pix - pix_base) * spp + s.
+struct WarmArgs {
+  uint32_t W, spp, seed0, row_begin, row_stride, pix_base;
+  uint64_t n;  // samples in the launch
+  uint32_t* out;
+};
+
+__global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+  for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < wa.n; i0 += stride) {
+    uint32_t x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t i = i0 + k < wa.n ? i0 + k : wa.n - 1;
+      const uint32_t pix = wa.pix_base + (uint32_t)(i / wa.spp), sm = (uint32_t)(i % wa.spp);
+      const uint32_t tr = pix / wa.W, xx = pix - tr * wa.W;
+      const uint32_t y = wa.row_begin + tr * wa.row_stride;
+      x[k] = wa.seed0 + (y * wa.W + xx) * wa.spp + sm;
+    }
+    ykd::mt_walk397x4(x);
+    if (i0 + 4 <= wa.n) {
+      *(uint4*)(wa.out + i0) = make_uint4(x[0], x[1], x[2], x[3]);
+    } else {
+      for (int k = 0; k < 4 && i0 + k < wa.n; ++k) wa.out[i0 + k] = x[k];
+    }
+  }
+}
+
+// kSceneInLds: the BVH nodes, the leaf-ordered sphere geometry and the leaf→tuple ids are copied
+// into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
+// ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
+template <bool kSceneInLds>
 __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ykbvh::Node* __restrict__ nodes = ka.nodes;
+  const SphereGeo* __restrict__ leaf_geo = ka.leaf_geo;
+  const uint32_t* __restrict__ leaf_ids = ka.leaf_ids;
+  if (kSceneInLds) {
+    const uint4* src[3] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids};
+    const uint32_t off[3] = {0u, ka.lds_geo_off, ka.lds_ids_off};
+    const uint32_t n16[3] = {ka.n_nodes * 4u, ka.nspheres * 2u, (ka.nspheres + 3u) / 4u};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      uint4* dst = (uint4*)(smem + off[k]);
+      for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlock) dst[i] = src[k][i];
+    }
+    __syncthreads();
+    nodes = (const ykbvh::Node*)smem;
+    leaf_geo = (const SphereGeo*)(smem + ka.lds_geo_off);
+    leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
+  }
+  int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlock]
 
   ykd::MtLane g;
   g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
   g.a0 = g.a1 = g.b = g.j = g.seed = 0;
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
 
-  const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
-  const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
-  const v3 lens_u = ld3(ka.cam.lens_u), lens_v = ld3(ka.cam.lens_v);
-  const double lens_r = ka.cam.lens_radius;
-
-  __shared__ int32_t s_stack[ykbvh::kMaxDepth][kBlock];  // per-lane BVH traversal stacks
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0;
 
   uint32_t pix = 0, s = 0, depth = 0, nstk = 0;
@@ -203,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
       base = __shfl(base, leader);
       const uint32_t mine = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
       if (mine >= ka.npix) break;
-      pix = mine;
+      pix = ka.pix_base + mine;
       s = 0;
       acc_r = acc_g = acc_b = 0.0;
       have_pixel = true;
@@ -214,10 +263,15 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
     if (!in_path) {
       const uint32_t tr = pix / ka.W, x = pix - tr * ka.W;
       const uint32_t y = ka.row_begin + tr * ka.row_stride;
-      ykd::mt_start(g, ka.seed0 + (y * ka.W + x) * ka.spp + s);  // uint32 wrap, :154-158
+      // seed (uint32 wrap, source.cpp:154-158); x_397 comes from yk_mt_warmup
+      ykd::mt_start_from(g, ka.seed0 + (y * ka.W + x) * ka.spp + s,
+                         ka.warm[(size_t)(pix - ka.pix_base) * ka.spp + s]);
       const double u = ((double)x + ykd::uniform(g, 0, 1)) / (double)ka.W;
       const double v = ((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1)) / (double)ka.H;
       // camera::get_ray (camera.hpp:29-32): llc + u*horizontal + v*vertical (- origin)
+      const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
+      const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
+      const double lens_r = ka.cam.lens_radius;
       d = ykd::sub(ykd::add(ykd::add(cam_llc, ykd::mul(cam_h, u)), ykd::mul(cam_v, v)), cam_o);
       o = cam_o;
       if (lens_r > 0) {  // thin-lens extension: random_in_unit_disk by rejection
@@ -227,6 +281,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
           py = ykd::uniform(g, -1, 1);
         } while (!(px * px + py * py < 1.0));
         const double rx = px * lens_r, ry = py * lens_r;
+        const v3 lens_u = ld3(ka.cam.lens_u), lens_v = ld3(ka.cam.lens_v);
         const v3 off = ykd::add(ykd::mul(lens_u, rx), ykd::mul(lens_v, ry));
         o = ykd::add(o, off);
         d = ykd::sub(d, off);
@@ -268,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         for (;;) {
           if (node >= 0) {
             ++n_node;
-            const ykbvh::Node nd = ka.nodes[node];
+            const ykbvh::Node nd = nodes[node];
             float tn[2], tf[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -284,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
             const bool h1 = tn[1] <= tf[1] && tf[1] >= tminf && tn[1] <= ustar_f;
             if (h0 && h1) {
               const bool first0 = tn[0] <= tn[1];
-              s_stack[sp][threadIdx.x] = first0 ? nd.child[1] : nd.child[0];
+              stk[sp * kBlock] = first0 ? nd.child[1] : nd.child[0];
               ++sp;
               node = first0 ? nd.child[0] : nd.child[1];
               continue;
@@ -296,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
           } else {
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
             for (uint32_t k = 0; k < cnt; ++k) {
-              const SphereGeo sg = ka.leaf_geo[first + k];
+              const SphereGeo sg = leaf_geo[first + k];
               ++n_test;
               // the reference's discriminant, bit for bit (sphere.hpp:29-34)
               const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
@@ -316,7 +371,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
                 ustar = ub;
                 ustar_f = (float)ub * (1.0f + 0x1p-20f);
               }
-              const uint32_t id = ka.leaf_ids[first + k];
+              const uint32_t id = leaf_ids[first + k];
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
                 uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
@@ -337,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
           }
           if (sp == 0) break;
           --sp;
-          node = s_stack[sp][threadIdx.x];
+          node = stk[sp * kBlock];
         }
         if (overflow) {
           linear = true;
@@ -481,7 +536,13 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
 struct ykgpu_context {
   int device = 0;
   int cus = 0;
-  int grid = 0;  // persistent blocks
+  int grid = 0;  // persistent blocks for the current scene
+  size_t scratch_lanes = 0;
+  bool scene_in_lds = false;
+  uint32_t lds_bytes = 0, lds_geo_off = 0, lds_ids_off = 0, lds_stack_off = 0, stack_depth = 0;
+  uint32_t n_nodes = 0;
+  uint32_t* d_warm = nullptr;  // x_397 per sample of one chunk
+  size_t warm_cap = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   SphereGeo* d_geo = nullptr;
@@ -530,9 +591,17 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
 
 int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
   const size_t lanes = (size_t)ctx->grid * kBlock;
-  if (!ctx->d_mt) YK_HIP(hipMalloc(&ctx->d_mt, lanes * ykd::kMtN * sizeof(uint32_t)));
+  if (lanes > ctx->scratch_lanes) {
+    (void)hipFree(ctx->d_mt);
+    (void)hipFree(ctx->d_ids);
+    ctx->d_mt = nullptr;
+    ctx->d_ids = nullptr;
+    ctx->id_stride = 0;
+    YK_HIP(hipMalloc(&ctx->d_mt, lanes * ykd::kMtN * sizeof(uint32_t)));
+    ctx->scratch_lanes = lanes;
+  }
   const uint32_t need = max_depth > kStackRegs ? max_depth : 1;
-  if (need > ctx->id_stride) {
+  if (need > ctx->id_stride || !ctx->d_ids) {
     if (ctx->d_ids) YK_HIP(hipFree(ctx->d_ids));
     ctx->d_ids = nullptr;
     YK_HIP(hipMalloc(&ctx->d_ids, lanes * need * sizeof(uint16_t)));
@@ -541,10 +610,24 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
   return YK_OK;
 }
 
+constexpr uint64_t kWarmChunkSamples = 1ull << 30;  // 4 GiB of x_397 per launch at most
+
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
   int rc = ensure_scratch(ctx, p->max_depth);
   if (rc) return rc;
+  const uint32_t npix_total = p->row_count * p->image_width;
+  const uint64_t total = (uint64_t)npix_total * p->samples_per_pixel;
+  const uint32_t chunk_pix =
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npix_total, kWarmChunkSamples / p->samples_per_pixel));
+  const size_t warm_need = (size_t)std::min<uint64_t>(total, (uint64_t)chunk_pix * p->samples_per_pixel);
+  if (warm_need > ctx->warm_cap) {
+    (void)hipFree(ctx->d_warm);
+    ctx->d_warm = nullptr;
+    ctx->warm_cap = 0;
+    YK_HIP(hipMalloc(&ctx->d_warm, warm_need * sizeof(uint32_t)));
+    ctx->warm_cap = warm_need;
+  }
   KernelArgs ka;
   ka.cam = ctx->cam;
   ka.W = p->image_width;
@@ -556,13 +639,18 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.row_count = p->row_count;
   ka.row_stride = p->row_stride;
   ka.nspheres = ctx->nspheres;
-  ka.npix = p->row_count * p->image_width;
   ka.flags = p->flags;
   ka.id_stride = ctx->id_stride;
+  ka.pad1 = 0;
+  ka.warm = ctx->d_warm;
   ka.t_min = p->t_min;
   ka.origin_bound = ctx->origin_bound;
   ka.bvh_root = ctx->bvh_root;
-  ka.pad0 = 0;
+  ka.n_nodes = ctx->n_nodes;
+  ka.lds_geo_off = ctx->lds_geo_off;
+  ka.lds_ids_off = ctx->lds_ids_off;
+  ka.lds_stack_off = ctx->lds_stack_off;
+  ka.stack_depth = ctx->stack_depth;
   ka.nodes = ctx->d_nodes;
   ka.leaf_geo = ctx->d_leaf_geo;
   ka.leaf_ids = ctx->d_leaf_ids;
@@ -574,15 +662,37 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.mt_scratch = ctx->d_mt;
   ka.id_scratch = ctx->d_ids;
   ka.counters = ctx->d_stats;
-  YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
+  WarmArgs wa;
+  wa.W = p->image_width;
+  wa.spp = p->samples_per_pixel;
+  wa.seed0 = p->seed0;
+  wa.row_begin = p->row_begin;
+  wa.row_stride = p->row_stride;
+  wa.out = ctx->d_warm;
   YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
   YK_HIP(hipEventRecord(ctx->ev0, st));
-  hipLaunchKernelGGL(yk_render_persistent, dim3(ctx->grid), dim3(kBlock), 0, st, ka);
-  YK_HIP(hipGetLastError());
+  uint32_t launches = 0;
+  for (uint32_t p0 = 0; p0 < npix_total; p0 += chunk_pix) {
+    const uint32_t cnt = std::min(chunk_pix, npix_total - p0);
+    wa.pix_base = p0;
+    wa.n = (uint64_t)cnt * p->samples_per_pixel;
+    const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * 32);
+    hipLaunchKernelGGL(yk_mt_warmup, dim3(wblocks), dim3(256), 0, st, wa);
+    YK_HIP(hipGetLastError());
+    ka.pix_base = p0;
+    ka.npix = cnt;
+    YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
+    if (ctx->scene_in_lds)
+      hipLaunchKernelGGL(yk_render_persistent<true>, dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+    else
+      hipLaunchKernelGGL(yk_render_persistent<false>, dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+    YK_HIP(hipGetLastError());
+    ++launches;
+  }
   YK_HIP(hipEventRecord(ctx->ev1, st));
   ctx->stats = yk_render_stats{};
-  ctx->stats.samples = (uint64_t)ka.npix * ka.spp;
-  ctx->stats.launches = 1;
+  ctx->stats.samples = total;
+  ctx->stats.launches = launches;
   ctx->stats.grid_blocks = (uint32_t)ctx->grid;
   ctx->stats_pending = true;
   return YK_OK;
@@ -641,10 +751,10 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   auto* ctx = new ykgpu_context();
   ctx->device = device;
   ctx->cus = prop.multiProcessorCount;
-  int per_cu = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent, kBlock, 0);
-  if (e != hipSuccess || per_cu < 1) per_cu = 1;
-  ctx->grid = per_cu * ctx->cus;
+  (void)hipFuncSetAttribute((const void*)yk_render_persistent<true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)yk_render_persistent<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_counter, 16) != hipSuccess ||
@@ -664,6 +774,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_mat);
   (void)hipFree(ctx->d_counter);
   (void)hipFree(ctx->d_stats);
+  (void)hipFree(ctx->d_warm);
   (void)hipFree(ctx->d_nodes);
   (void)hipFree(ctx->d_leaf_geo);
   (void)hipFree(ctx->d_leaf_ids);
@@ -731,6 +842,23 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   ctx->bvh_root = bvh.root;
   ctx->bvh_depth = bvh.depth;
   ctx->origin_bound = bvh.origin_bound;
+  ctx->n_nodes = (uint32_t)bvh.nodes.size();
+  // LDS layout: [nodes][leaf geometry][leaf ids][traversal stacks]
+  auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t scene_bytes = a16(ctx->n_nodes * sizeof(ykbvh::Node)) + a16(count * sizeof(SphereGeo)) +
+                             a16(count * sizeof(uint32_t));
+  ctx->scene_in_lds = scene_bytes <= 64 * 1024;
+  ctx->stack_depth = bvh.depth + 1;
+  ctx->lds_geo_off = (uint32_t)a16(ctx->n_nodes * sizeof(ykbvh::Node));
+  ctx->lds_ids_off = ctx->lds_geo_off + (uint32_t)a16(count * sizeof(SphereGeo));
+  ctx->lds_stack_off = ctx->scene_in_lds ? (uint32_t)scene_bytes : 0u;
+  ctx->lds_bytes = ctx->lds_stack_off + ctx->stack_depth * kBlock * (uint32_t)sizeof(int32_t);
+  int per_cu = 0;
+  hipError_t e = ctx->scene_in_lds
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<true>, kBlock, ctx->lds_bytes)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<false>, kBlock, ctx->lds_bytes);
+  if (e != hipSuccess || per_cu < 1) per_cu = 1;
+  ctx->grid = per_cu * ctx->cus;
   YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));
   ctx->nspheres = count;
   ctx->cam = *camera;
