@@ -22,7 +22,7 @@ print(json.dumps({"ms": min(ts), "segs": st["segments"] / st["samples"]}))
 ''' % ROOT
 variants = [("base", os.path.join(ROOT, "uecraytracing_amd/lib/libykgpu.so"))]
 for m in sys.argv[2:] or ["1", "2", "3"]:
-    variants.append((f"ablate{m}", os.path.join(ROOT, f"uecraytracing_amd/lib/abl/libykgpu_{m}.so")))
+    variants.append((f"v_{m}", os.path.join(ROOT, f"uecraytracing_amd/lib/abl/libykgpu_{m}.so")))
 spp = sys.argv[1] if len(sys.argv) > 1 else "64"
 for rnd in range(2):
     for name, lib in variants:

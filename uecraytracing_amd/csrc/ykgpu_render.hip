@@ -70,7 +70,26 @@ struct alignas(16) SphereMat {
 static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 
 constexpr int kBlock = 256;
-constexpr int kCounters = 8;
+constexpr int kCounters = 16;
+
+// Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
+// points, summed per phase into counters[8..13] (refill, start, traversal, candidates, shade,
+// path end).
+#if YK_ABLATE & 8
+#define YK_STAMP(k)                                                                  \
+  do {                                                                               \
+    uint64_t t_;                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    st_acc[k] += t_ - st_prev;                                                       \
+    st_prev = t_;                                                                    \
+  } while (0)
+#else
+#define YK_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 
@@ -236,6 +255,10 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
 
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0;
 
+#if YK_ABLATE & 8
+  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#endif
   uint32_t pix = 0, s = 0, depth = 0, nstk = 0;
   uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // newest attenuation id in st0's low half
   double acc_r = 0, acc_g = 0, acc_b = 0;
@@ -258,6 +281,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
       have_pixel = true;
       in_path = false;
     }
+    YK_STAMP(0);
 
     // ---- start sample s of the pixel: seed, jitter, camera ray (source.cpp:154-165) ------
     if (!in_path) {
@@ -290,27 +314,28 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
       nstk = 0;
       in_path = true;
     }
+    YK_STAMP(1);
 
     // ---- one segment of ray_color (raytracer.hpp:19-37) ----------------------------------
-    bool ended = false;
-    double L_r = 0, L_g = 0, L_b = 0;
-    if (depth == 0) {
-      ended = true;  // :23 black
-    } else {
+    // (a) closest hit: hittable_list::hit_impl (hittable_list.hpp:32-58) over
+    //     sphere::hit_impl (sphere.hpp:25-48): tuple order, t_max shrinking to the last
+    //     accepted root, so the closest hit wins and an exact tie goes to the later sphere.
+    const bool alive = depth != 0;  // depth == 0 → black (raytracer.hpp:23)
+    Hit hit{INFINITY, -1, 0, 0};
+    if (alive) {
       ++n_seg;
-      // hittable_list::hit_impl (hittable_list.hpp:32-58) over sphere::hit_impl
-      // (sphere.hpp:25-48): tuple order, t_max shrinks to the last accepted root, so the
-      // closest hit wins and an exact tie goes to the later sphere.
       const double a = ykd::len2(d);
       const double onorm = fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z)));
-      Hit hit{INFINITY, -1, 0, 0};
       bool linear = (ka.flags & kFlagLinearScan) || !(a > 0 && a < INFINITY) ||
                     !(onorm <= ka.origin_bound);
       if (!linear) {
-        // ---- BVH traversal: cull conservatively, keep every sphere whose exact root could
-        //      be the minimum -------------------------------------------------
-        const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+        // BVH traversal: cull conservatively, keep every sphere whose exact root could be
+        // the minimum.  Slab distances as one FMA each,
+        // t = lo*(1/d) - o*(1/d): error relative 2^-22 plus an origin perturbation of
+        // 2^-23|o| (< delta/4), inside the culling contract of yk_bvh.hpp.  This is culling
+        // arithmetic only, so explicit FMAs are fine here.
         const float ix = safe_rcp((float)d.x), iy = safe_rcp((float)d.y), iz = safe_rcp((float)d.z);
+        const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
         const double ia = 1.0 / a;
         const float tminf = (float)ka.t_min;
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
@@ -321,19 +346,19 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         int32_t node = ka.bvh_root;
         uint32_t sp = 0;
         for (;;) {
-          if (node >= 0) {
+        if (node >= 0) {
             ++n_node;
             const ykbvh::Node nd = nodes[node];
             float tn[2], tf[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-              const float ax = (nd.lo_x[k] - ox) * ix, bx = (nd.hi_x[k] - ox) * ix;
-              const float ay = (nd.lo_y[k] - oy) * iy, by = (nd.hi_y[k] - oy) * iy;
-              const float az = (nd.lo_z[k] - oz) * iz, bz = (nd.hi_z[k] - oz) * iz;
+              const float ax = __builtin_fmaf(nd.lo_x[k], ix, -oix), bx = __builtin_fmaf(nd.hi_x[k], ix, -oix);
+              const float ay = __builtin_fmaf(nd.lo_y[k], iy, -oiy), by = __builtin_fmaf(nd.hi_y[k], iy, -oiy);
+              const float az = __builtin_fmaf(nd.lo_z[k], iz, -oiz), bz = __builtin_fmaf(nd.hi_z[k], iz, -oiz);
               const float n0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
               const float f0 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-              tn[k] = n0 - fabsf(n0) * 0x1p-20f;  // relax by the float error bound
-              tf[k] = f0 + fabsf(f0) * 0x1p-20f;
+              tn[k] = __builtin_fmaf(-fabsf(n0), 0x1p-20f, n0);  // relax by the error bound
+              tf[k] = __builtin_fmaf(fabsf(f0), 0x1p-20f, f0);
             }
             const bool h0 = tn[0] <= tf[0] && tf[0] >= tminf && tn[0] <= ustar_f;
             const bool h1 = tn[1] <= tf[1] && tf[1] >= tminf && tn[1] <= ustar_f;
@@ -394,6 +419,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
           --sp;
           node = stk[sp * kBlock];
         }
+        YK_STAMP(2);
         if (overflow) {
           linear = true;
         } else {
@@ -410,33 +436,50 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         ++n_lin;
       }
       n_sqrt += hit.sqrts;
-      const double T = hit.T;
-      const int hid = hit.hid;
+    }
+    YK_STAMP(3);
 
+    // (b) shade.  Every live lane needs exactly one vector normalisation here — the sky's
+    //     normalized(dir) (raytracer.hpp:35), lambertian's random_unit_vector
+    //     (material.hpp:33-36), metal's / dielectric's normalized(dir) — so the Newton square
+    //     root of that length runs once, with all those lanes together, instead of once per
+    //     branch.  Each lane's own operation order is unchanged.
+    bool ended = !alive;
+    double L_r = 0, L_g = 0, L_b = 0;
+    if (alive) {
+      const int hid = hit.hid;
+      const double T = hit.T;
+      SphereGeo sg{0, 0, 0, 0};
+      SphereMat m{};
+      v3 p{0, 0, 0}, nrm{0, 0, 0};
+      bool front = false;
+      v3 vn = d;
+      if (hid >= 0) {
+        sg = ka.geo[hid];
+        m = ka.mat[hid];
+        // hit record (sphere.hpp:41-45, hittable.hpp:23-27)
+        p = ykd::add(o, ykd::mul(d, T));
+        const v3 outward = ykd::divs(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
+        front = ykd::dot(d, outward) < 0;
+        nrm = front ? outward : ykd::neg(outward);
+        if (m.kind == YK_MATERIAL_LAMBERTIAN) vn = ykd::random_vec(g, -1, 1);  // vec3.hpp:134-142
+      }
+      const double len = ykd::nsqrt(ykd::len2(vn));  // vec3::length(), vec3.hpp:127
       if (hid < 0) {
         // sky (raytracer.hpp:35-36): t = (normalized(dir).y + 1)/2, lerp white → (.5,.7,1)
-        const double t = (d.y / ykd::nsqrt(ykd::len2(d)) + 1.0) / 2;
+        const double t = (d.y / len + 1.0) / 2;
         L_r = (1.0 - t) * 1.0 + t * 0.5;
         L_g = (1.0 - t) * 1.0 + t * 0.7;
         L_b = (1.0 - t) * 1.0 + t * 1.0;
         ended = true;
       } else {
-        const SphereGeo sg = ka.geo[hid];
-        const SphereMat m = ka.mat[hid];
-        // hit record (sphere.hpp:41-45, hittable.hpp:23-27)
-        const v3 p = ykd::add(o, ykd::mul(d, T));
-        const v3 outward = ykd::divs(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
-        const bool front = ykd::dot(d, outward) < 0;
-        const v3 nrm = front ? outward : ykd::neg(outward);
         bool scattered = true, push = true;
         v3 nd;
         if (m.kind == YK_MATERIAL_LAMBERTIAN) {  // material.hpp:50-59
-          v3 ru = ykd::random_vec(g, -1, 1);
-          ru = ykd::divs(ru, ykd::nsqrt(ykd::len2(ru)));
-          nd = ykd::add(nrm, ru);
+          nd = ykd::add(nrm, ykd::divs(vn, len));
           if (ykd::near_zero(nd)) nd = nrm;
         } else if (m.kind == YK_MATERIAL_METAL) {  // material.hpp:67-75 (+ fuzz extension)
-          nd = ykd::reflect(ykd::normalized(d), nrm);
+          nd = ykd::reflect(ykd::divs(d, len), nrm);
           if (m.fuzz > 0) {  // random_in_unit_sphere, material.hpp:27-30
             v3 ru = ykd::random_vec(g, -1, 1);
             ru = ykd::divs(ru, ykd::nsqrt(ykd::len2(ru)));
@@ -447,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         } else {  // dielectric extension (attenuation (1,1,1): multiplying by 1.0 is exact)
           push = false;
           const double ratio = front ? (1.0 / m.ior) : m.ior;
-          const v3 unit = ykd::normalized(d);
+          const v3 unit = ykd::divs(d, len);
           double ct = ykd::dot(ykd::neg(unit), nrm);
           if (!(ct < 1.0)) ct = 1.0;
           const double sn = ykd::nsqrt(1.0 - ct * ct);
@@ -477,6 +520,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         }
       }
     }
+    YK_STAMP(4);
 
     if (ended) {
       // unwind: attenuation_k * (...) from the deepest scatter outwards (raytracer.hpp:31)
@@ -516,8 +560,13 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         have_pixel = false;
       }
     }
+    YK_STAMP(5);
   }
 
+#if YK_ABLATE & 8
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&ka.counters[8 + k], (unsigned long long)st_acc[k]);
+#endif
   if (ka.flags & YK_FLAG_COUNT_WORK) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
     atomicAdd(&ka.counters[1], (unsigned long long)n_test);
@@ -707,6 +756,7 @@ int finish_stats(ykgpu_context* ctx) {
   YK_HIP(hipMemcpy(c, ctx->d_stats, sizeof(c), hipMemcpyDeviceToHost));
   ctx->stats.node_visits = c[4];
   ctx->stats.linear_scans = c[5];
+  for (int k = 0; k < 6; ++k) ctx->stats.phase_cycles[k] = c[8 + k];
   ctx->stats.kernel_ms = ms;
   ctx->stats.segments = c[0];
   ctx->stats.sphere_tests = c[1];

@@ -93,12 +93,15 @@ class RenderStats(ctypes.Structure):
         ("mt_fallbacks", ctypes.c_uint64),
         ("node_visits", ctypes.c_uint64),
         ("linear_scans", ctypes.c_uint64),
+        ("phase_cycles", ctypes.c_uint64 * 6),
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
     ]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_}
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["phase_cycles"] = list(self.phase_cycles)
+        return d
 
 
 assert ctypes.sizeof(Sphere) == 80
