@@ -30,7 +30,36 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/sec at 1920x1080x512spp (~500 spheres); per-pixel RMSE vs CPU"
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP32 vector 157.3 TF / 2, MI355X_MICROARCH.md)
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
-FLOPS_PER_SPHERE_TEST = 17    # sphere.hpp:29-33 discriminant: 3 sub, 6 mul+4 add (dots), 1 sub, 2 mul+1 sub
+# Algorithmic FP64 flops per work unit, counted from the reference's arithmetic:
+FLOPS_PER_SPHERE_TEST = 17    # sphere.hpp:29-33 discriminant: 3 sub, 2 dots (3 mul+2 add), 1 sub, 2 mul+1 sub
+FLOPS_PER_ROOT = 4            # sphere.hpp:36-39: (-hb -/+ sq) / a, one or two roots
+FLOPS_PER_NEWTON_ITER = 3     # math.hpp:14-17: s/x, x + ., ./2
+FLOPS_PER_SEGMENT = 40        # |d|^2, hit record (p, normal, face: 17), normalize (8), scatter (~10)
+FLOPS_PER_SAMPLE = 30         # jitter + camera ray (24), accumulate + attenuation products (~6)
+
+
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+
+
+def pmc_facts(workload=None):
+    """Counter facts of the same workload from the committed rocprofv3 --pmc passes
+    (tools/pmc_profile.sh + tools/pmc_summary.py → profiles/pmc_summary.json), or None."""
+    if not os.path.exists(PMC_SUMMARY):
+        return None
+    with open(PMC_SUMMARY) as f:
+        rec = json.load(f)
+    if workload is not None and rec.get("workload") != workload:
+        return None
+    keep = ("source", "workload", "mean_ms", "valu_busy", "valu_lane_utilization",
+            "SQ_WAIT_ANY_frac", "SQ_WAIT_INST_ANY_frac", "hbm_bytes_per_launch",
+            "fp64_flops_hw_per_launch")
+    return {k: rec[k] for k in keep if k in rec}
+
+
+def fp64_flops(st):
+    return (st["sphere_tests"] * FLOPS_PER_SPHERE_TEST + st["sqrt_calls"] * FLOPS_PER_ROOT
+            + st["newton_calls"] + st["newton_iters"] * FLOPS_PER_NEWTON_ITER
+            + st["segments"] * FLOPS_PER_SEGMENT + st["samples"] * FLOPS_PER_SAMPLE)
 
 
 def parse():
@@ -64,6 +93,7 @@ def main():
 
     import uecraytracing_amd as yk
     from uecraytracing_amd.records import image_height_for, make_params
+    from uecraytracing_amd.tiles import TileGather, tile_rows
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -75,18 +105,14 @@ def main():
     W, spp, depth = args.width, args.spp, args.depth
     H = image_height_for(W)
     spheres, cam = yk.build_scene(args.scene, args.scene_seed)
-    rows_mine = len(range(rank, H, world))
-    rows_max = -(-H // world)
-    params = make_params(W, H, spp, depth, args.seed0, rows=(rank, rows_mine, world), flags=1)
+    rows = tile_rows(rank, world, H)
+    rows_mine = rows[1]
+    params = make_params(W, H, spp, depth, args.seed0, rows=rows, flags=1)
 
     ren = yk.Renderer(local)
     ren.set_scene(spheres, cam)  # world + camera uploaded to HBM before any timing
     stream = torch.cuda.Stream(device=dev)
-    tile = torch.zeros((rows_max, W, 3), dtype=torch.uint8, device=dev)
-    gathered = torch.empty((world, rows_max, W, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
-    # row r of the image is row r // world of rank r % world's tile
-    perm = torch.tensor([(r % world) * rows_max + r // world for r in range(H)], device=dev)
-    image = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+    tg = TileGather(rank, world, H, W, dev)  # tile, gather buffers and the assembled image
     ev = []
 
     def step(timed):
@@ -94,16 +120,11 @@ def main():
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-            ren.render_async(params, tile.data_ptr(), stream.cuda_stream)
+            ren.render_async(params, tg.tile.data_ptr(), stream.cuda_stream)
             if timed:
                 e1.record(stream)
                 ev.append((e0, e1))
-            if world > 1:
-                dist.gather(tile, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-                if rank == 0:
-                    torch.index_select(gathered.reshape(world * rows_max, W, 3), 0, perm, out=image)
-            else:
-                image.copy_(tile[:H])
+            tg.gather()  # RCCL gather to rank 0 + de-interleave (world > 1)
 
     for _ in range(args.warmup):
         step(False)
@@ -129,17 +150,14 @@ def main():
     total_samples = W * H * spp
     value = total_samples * args.steps / elapsed / 1e6
 
-    # roofline of the dominant kernel (this rank's launch)
-    flops = st["sphere_tests"] * FLOPS_PER_SPHERE_TEST
+    # roofline of the dominant kernel (this rank's launch): algorithmic FP64 work of the
+    # reference arithmetic actually executed, from the kernel's own unit counters
+    flops = fp64_flops(st)
     achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
     hbm_bytes = rows_mine * W * 3 + len(spheres) * 96  # RGB8 out + scene in (algorithmic)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            rec = json.load(f)
-        if rec.get("workload") == f"{args.scene}{args.scene_seed}_{W}x{H}x{spp}_d{depth}_n{world}":
-            traffic = rec.get("hbm_bytes_per_launch")
+    workload = f"{args.scene}{args.scene_seed}_{W}x{H}x{spp}_d{depth}_n{world}"
+    facts = pmc_facts(workload)
+    traffic = facts.get("hbm_bytes_per_launch") if facts else None
 
     result = {
         "metric": METRIC,
@@ -169,8 +187,14 @@ def main():
             "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 4),
             "traffic": traffic,
             "kernel_ms": round(kernel_ms, 3),
-            "algorithmic": f"{FLOPS_PER_SPHERE_TEST} FP64 flop per ray-sphere discriminant x "
-                           f"{st['sphere_tests']} tests per launch",
+            "algorithmic": (f"FP64 flops of the reference arithmetic executed per launch = "
+                            f"{FLOPS_PER_SPHERE_TEST}/sphere test x {st['sphere_tests']} + "
+                            f"{FLOPS_PER_ROOT}/exact root x {st['sqrt_calls']} + math::sqrt "
+                            f"(1/call x {st['newton_calls']} + {FLOPS_PER_NEWTON_ITER}/iteration x "
+                            f"{st['newton_iters']}) + {FLOPS_PER_SEGMENT}/segment x "
+                            f"{st['segments']} + {FLOPS_PER_SAMPLE}/sample x {st['samples']} = "
+                            f"{flops:.4g}"),
+            "pmc": facts,
             "hbm": {"achieved_gbps": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 4),
                     "peak_gbps": HBM_PEAK_GBPS,
                     "frac": hbm_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
@@ -194,7 +218,7 @@ def main():
         cpu_rgb, _, _, _ = oracle_lib.render(spheres, cam, cp, nthreads=nthreads)
         dt = time.perf_counter() - t
         n = len(rows) * W * spp
-        gpu_rows = image[::args.cpu_row_step].cpu().numpy()
+        gpu_rows = tg.image[::args.cpu_row_step].cpu().numpy()
         diff = (gpu_rows.astype(np.float64) - cpu_rgb.astype(np.float64)) / 255.0
         result["cpu_baseline"] = {
             "value": round(n / dt / 1e6, 4),

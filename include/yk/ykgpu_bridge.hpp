@@ -1,0 +1,195 @@
+// yk/ykgpu_bridge.hpp — the host-side adapter between a yk scene and the C-ABI (ykgpu.h).
+//
+// Flattens a world into yk_sphere records in tuple order (the order defines rec.id, the
+// closest-hit tie-break and the scatter dispatch: /root/reference/yk/hittable_list.hpp:32-73)
+// with std::apply over hittable_list::objects, and copies camera<T>'s public members
+// (camera.hpp:34-37).  Only the public data members the reference's own types expose are
+// read, so the same template compiles against either
+//   * include/yk/scene.hpp (this repository's scene API), or
+//   * the reference's yk/hittable_list.hpp + yk/sphere.hpp + yk/material.hpp + yk/camera.hpp
+// — i.e. the reference's source.cpp can hand its world to the GPU unchanged.
+//
+// Then ykgpu::renderer runs the render loop of source.cpp:122-172 on the device and returns
+// the image_t bytes (source.cpp:70-71: row-major, row 0 at the top, RGB interleaved).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <type_traits>
+#include <vector>
+
+#include "../ykgpu.h"
+
+namespace ykgpu {
+
+namespace detail {
+template <class M>
+concept has_fuzz = requires(const M& m) { m.fuzz; };
+template <class M>
+concept has_ior = requires(const M& m) { m.ior; };
+template <class W>
+concept tuple_world = requires(const W& w) { std::tuple_size<std::decay_t<decltype(w.objects)>>::value; };
+template <class C>
+concept thin_lens = requires(const C& c) { c.lens_radius; c.lens_u; c.lens_v; };
+
+template <class V>
+void put3(double* dst, const V& v) {
+  dst[0] = static_cast<double>(v.x);
+  dst[1] = static_cast<double>(v.y);
+  dst[2] = static_cast<double>(v.z);
+}
+template <class C>
+void put_rgb(double* dst, const C& c) {
+  dst[0] = static_cast<double>(c.r);
+  dst[1] = static_cast<double>(c.g);
+  dst[2] = static_cast<double>(c.b);
+}
+}  // namespace detail
+
+// material.hpp:37-53 (lambertian) — the reference's and ours.
+template <class U>
+void set_material(yk_sphere& r, const yk::lambertian<U>& m) {
+  r.material = YK_MATERIAL_LAMBERTIAN;
+  detail::put_rgb(r.albedo, m.albedo);
+}
+// material.hpp:55-69 (metal); fuzz only exists in the extension.
+template <class U>
+void set_material(yk_sphere& r, const yk::metal<U>& m) {
+  r.material = YK_MATERIAL_METAL;
+  detail::put_rgb(r.albedo, m.albedo);
+  if constexpr (detail::has_fuzz<yk::metal<U>>) r.fuzz = static_cast<double>(m.fuzz);
+}
+#ifdef YK_SCENE_HAS_EXTENSIONS
+template <class U>
+void set_material(yk_sphere& r, const yk::dielectric<U>& m) {
+  r.material = YK_MATERIAL_DIELECTRIC;
+  r.albedo[0] = r.albedo[1] = r.albedo[2] = 1.0;
+  r.ior = static_cast<double>(m.ior);
+}
+#endif
+
+// sphere.hpp:16-23
+template <class S>
+yk_sphere to_record(const S& s) {
+  yk_sphere r;
+  std::memset(&r, 0, sizeof r);
+  detail::put3(r.center, s.center);
+  r.radius = static_cast<double>(s.radius);
+  set_material(r, s.material);
+  return r;
+}
+
+// hittable_list<T, Hs...>: tuple order
+template <class World>
+  requires detail::tuple_world<World>
+std::vector<yk_sphere> flatten(const World& w) {
+  std::vector<yk_sphere> out;
+  std::apply([&](const auto&... s) { (out.push_back(to_record(s)), ...); }, w.objects);
+  return out;
+}
+
+#ifdef YK_SCENE_HAS_EXTENSIONS
+// sphere_list<T>: insertion order
+template <class T>
+std::vector<yk_sphere> flatten(const yk::sphere_list<T>& w) {
+  std::vector<yk_sphere> out;
+  out.reserve(w.objects.size());
+  for (const auto& e : w.objects) {
+    yk_sphere r;
+    std::memset(&r, 0, sizeof r);
+    detail::put3(r.center, e.center);
+    r.radius = static_cast<double>(e.radius);
+    detail::put_rgb(r.albedo, e.albedo);
+    r.fuzz = static_cast<double>(e.fuzz);
+    r.ior = static_cast<double>(e.ior);
+    using K = typename yk::sphere_list<T>::kind;
+    r.material = e.k == K::lambertian ? YK_MATERIAL_LAMBERTIAN
+                 : e.k == K::metal    ? YK_MATERIAL_METAL
+                                      : YK_MATERIAL_DIELECTRIC;
+    out.push_back(r);
+  }
+  return out;
+}
+#endif
+
+// camera.hpp:34-37 (+ the thin-lens extension when present)
+template <class Cam>
+yk_camera camera_record(const Cam& c) {
+  yk_camera r;
+  std::memset(&r, 0, sizeof r);
+  detail::put3(r.origin, c.origin);
+  detail::put3(r.lower_left_corner, c.lower_left_corner);
+  detail::put3(r.horizontal, c.horizontal);
+  detail::put3(r.vertical, c.vertical);
+  if constexpr (detail::thin_lens<Cam>) {
+    detail::put3(r.lens_u, c.lens_u);
+    detail::put3(r.lens_v, c.lens_v);
+    r.lens_radius = static_cast<double>(c.lens_radius);
+  }
+  return r;
+}
+
+struct error : std::runtime_error {
+  int code;
+  error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+inline void check(int rc, const char* where) {
+  if (rc != YK_OK) throw error(rc, std::string(where) + ": " + ykgpu_last_error());
+}
+
+// One device context: the render loop of source.cpp:122-172 on the GPU.
+class renderer {
+ public:
+  explicit renderer(int device = 0) { check(ykgpu_context_create(device, &ctx_), "ykgpu_context_create"); }
+  ~renderer() { ykgpu_context_destroy(ctx_); }
+  renderer(const renderer&) = delete;
+  renderer& operator=(const renderer&) = delete;
+
+  template <class World, class Cam>
+  void set_scene(const World& world, const Cam& cam) {
+    const std::vector<yk_sphere> s = flatten(world);
+    const yk_camera c = camera_record(cam);
+    check(ykgpu_set_scene(ctx_, s.data(), (uint32_t)s.size(), &c), "ykgpu_set_scene");
+  }
+
+  // already-flattened records (e.g. yk_scene_build output)
+  void set_records(const std::vector<yk_sphere>& s, const yk_camera& c) {
+    check(ykgpu_set_scene(ctx_, s.data(), (uint32_t)s.size(), &c), "ykgpu_set_scene");
+  }
+
+  // image_t bytes of the whole image: W*H*3, row 0 at the top (source.cpp:70-71,224-226)
+  std::vector<uint8_t> render(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
+                              uint32_t seed0, double t_min = 0.001) {
+    yk_render_params p;
+    std::memset(&p, 0, sizeof p);
+    p.image_width = width;
+    p.image_height = height;
+    p.samples_per_pixel = spp;
+    p.max_depth = max_depth;
+    p.seed0 = seed0;
+    p.row_begin = 0;
+    p.row_count = height;
+    p.row_stride = 1;
+    p.precision = YK_PRECISION_FP64;
+    p.rng = YK_RNG_MT19937;
+    p.t_min = t_min;
+    std::vector<uint8_t> img((size_t)width * height * 3);
+    check(ykgpu_render(ctx_, &p, img.data()), "ykgpu_render");
+    return img;
+  }
+
+  yk_render_stats stats() {
+    yk_render_stats s;
+    check(ykgpu_get_stats(ctx_, &s), "ykgpu_get_stats");
+    return s;
+  }
+
+ private:
+  ykgpu_context* ctx_ = nullptr;
+};
+
+}  // namespace ykgpu

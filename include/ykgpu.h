@@ -116,6 +116,8 @@ typedef struct yk_render_stats {
   uint64_t mt_fallbacks;   /* samples that needed the full 624-word MT state           */
   uint64_t node_visits;    /* BVH inner nodes visited (flag COUNT_WORK)                */
   uint64_t linear_scans;   /* segments served by the exact linear scan (flag COUNT_WORK)*/
+  uint64_t newton_calls;   /* math::sqrt evaluations (flag COUNT_WORK)                 */
+  uint64_t newton_iters;   /* math::sqrt loop iterations (flag COUNT_WORK)             */
   uint64_t phase_cycles[6];/* diagnostic builds only (YK_ABLATE & 8): wave-cycles in refill,
                               sample start, traversal, candidates, shading, path end      */
   uint32_t launches;       /* path-tracing launches in the call                        */

@@ -1,4 +1,7 @@
-"""Summarise tools/pmc_profile.sh output: per-kernel counters averaged per dispatch."""
+"""Summarise tools/pmc_profile.sh output for one kernel: counters per dispatch and derived
+metrics (gfx950 corrections per MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half of a wide
+stream; GRBM_GUI_ACTIVE sums the 8 XCDs; SQ_* cycle counters are quad-cycles).
+usage: python tools/pmc_summary.py <pmc dir> [kernel-substring] [workload-tag] [out.json]"""
 import collections
 import csv
 import glob
@@ -8,6 +11,7 @@ import sys
 
 d = sys.argv[1]
 kern = sys.argv[2] if len(sys.argv) > 2 else "yk_render_persistent"
+workload = sys.argv[3] if len(sys.argv) > 3 else None
 agg = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 dur = []
@@ -21,16 +25,23 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_kernel_trace.csv"))):
         if kern in r["Kernel_Name"]:
             dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
 per = {k: v / len(disp[k]) for k, v in agg.items()}
-out = {"kernel": kern, "dispatches_profiled": len(dur), "mean_ms": sum(dur) / max(1, len(dur)), "counters_per_dispatch": per}
+out = {"source": f"rocprofv3 --kernel-trace --pmc (4 passes), {d}", "kernel": kern,
+       "workload": workload, "dispatches_profiled": len(dur),
+       "mean_ms": sum(dur) / max(1, len(dur)), "counters_per_dispatch": per}
 if "SQ_THREAD_CYCLES_VALU" in per and "SQ_ACTIVE_INST_VALU" in per:
     out["valu_lane_utilization"] = per["SQ_THREAD_CYCLES_VALU"] / (per["SQ_ACTIVE_INST_VALU"] * 64)
+if "SQ_ACTIVE_INST_VALU" in per and "GRBM_GUI_ACTIVE" in per:
+    cycles = per["GRBM_GUI_ACTIVE"] / 8  # per XCD
+    out["valu_busy"] = per["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * cycles)
 if "SQ_WAVE_CYCLES" in per:
-    wc = per["SQ_WAVE_CYCLES"]
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
         if k in per:
-            out[k + "_frac"] = per[k] / wc
-if "FETCH_SIZE" in per:
-    out["hbm_bytes_fetch_corrected"] = per["FETCH_SIZE"] * 1024 * 2  # gfx950: FETCH_SIZE reads 1/2 (MICROARCH §HBM)
-if "WRITE_SIZE" in per:
-    out["hbm_bytes_write"] = per["WRITE_SIZE"] * 1024
-print(json.dumps(out, indent=1))
+            out[k + "_frac"] = per[k] / per["SQ_WAVE_CYCLES"]
+if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+    out["hbm_bytes_per_launch"] = per["FETCH_SIZE"] * 1024 * 2 + per["WRITE_SIZE"] * 1024
+if "SQ_INSTS_VALU_FLOPS_FP64" in per:
+    out["fp64_flops_hw_per_launch"] = per["SQ_INSTS_VALU_FLOPS_FP64"]
+js = json.dumps(out, indent=1)
+if len(sys.argv) > 4:
+    open(sys.argv[4], "w").write(js + "\n")
+print(js)

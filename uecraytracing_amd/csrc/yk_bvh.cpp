@@ -38,6 +38,7 @@ struct Builder {
   std::vector<Node> nodes;
   bool median_only = false;
   uint32_t max_depth = 0;
+  Options opt;
 
   Box bounds(uint32_t b, uint32_t e) const {
     Box r;
@@ -48,7 +49,7 @@ struct Builder {
   // returns a child code for the subtree over idx[b, e)
   int32_t rec(uint32_t b, uint32_t e, uint32_t depth) {
     const uint32_t n = e - b;
-    if (n <= kMaxLeaf) {
+    if (n <= opt.max_leaf) {
       max_depth = std::max(max_depth, depth);
       return ~int32_t((b << 4) | n);
     }
@@ -60,9 +61,9 @@ struct Builder {
     uint32_t mid = b + n / 2;
     const double ext = cb.hi[axis] - cb.lo[axis];
     if (!median_only && ext > 0) {
-      constexpr int kBins = 16;
-      Box bb[kBins];
-      uint32_t cnt[kBins] = {};
+      const int kBins = std::min(std::max(opt.bins, 2), 256);
+      std::vector<Box> bb(kBins);
+      std::vector<uint32_t> cnt(kBins, 0);
       auto bin_of = [&](uint32_t s) {
         int q = int((cent[3 * s + axis] - cb.lo[axis]) / ext * kBins);
         return std::min(std::max(q, 0), kBins - 1);
@@ -121,7 +122,8 @@ struct Builder {
 
 }  // namespace
 
-Built build(const double* centers, const double* radii, uint32_t n, double camera_extent) {
+Built build(const double* centers, const double* radii, uint32_t n, double camera_extent,
+            const Options& opt) {
   Built out;
   double ext = camera_extent;
   for (uint32_t i = 0; i < n; ++i)
@@ -133,6 +135,7 @@ Built build(const double* centers, const double* radii, uint32_t n, double camer
     Builder bd;
     bd.c = centers;
     bd.median_only = attempt == 1;
+    bd.opt = opt;
     bd.sbox.resize(n);
     bd.cent.assign(centers, centers + 3 * size_t(n));
     bd.idx.resize(n);

@@ -35,10 +35,14 @@ struct Built {
   float delta = 0;              // box growth
 };
 
-// centers: 3 doubles per sphere; radii may be negative (hollow shells: |r| is used).
-Built build(const double* centers, const double* radii, uint32_t n, double camera_extent);
+struct Options {
+  uint32_t max_leaf = 2;  // spheres per leaf (<= 15); 2 measured best on the final scene
+  int bins = 16;          // SAH bins per split
+};
 
-constexpr uint32_t kMaxLeaf = 4;
+// centers: 3 doubles per sphere; radii may be negative (hollow shells: |r| is used).
+Built build(const double* centers, const double* radii, uint32_t n, double camera_extent,
+            const Options& opt = Options());
 constexpr uint32_t kMaxDepth = 32;  // traversal stack capacity (device, LDS)
 
 }  // namespace ykbvh

@@ -47,6 +47,21 @@ __device__ __forceinline__ double nsqrt(double s) {
   return x;
 }
 
+// Same, counting calls and loop iterations (work counters of the roofline model).
+__device__ __forceinline__ double nsqrt_c(double s, uint32_t& calls, uint32_t& iters) {
+  ++calls;
+#if YK_ABLATE & 2
+  return sqrt(s);
+#endif
+  double x = s / 2.0, prev = 0.0;
+  for (int guard = 0; x != prev && guard < 4096; ++guard) {
+    prev = x;
+    x = (x + s / x) / 2.0;
+    ++iters;
+  }
+  return x;
+}
+
 __device__ __forceinline__ v3 normalized(v3 a) { return divs(a, nsqrt(len2(a))); }  // :127,132
 // reflect(): vec3.hpp:199-202, v - (2*dot(v,n))*n
 __device__ __forceinline__ v3 reflect(v3 v, v3 n) { return sub(v, mul(n, 2.0 * dot(v, n))); }

@@ -122,6 +122,7 @@ struct Hit {
   double T;
   int hid;
   uint32_t tests, sqrts;
+  uint32_t ncalls, nits;  // math::sqrt calls / loop iterations
 };
 
 // The reference's closest-hit scan verbatim (hittable_list.hpp:32-58 over sphere.hpp:25-48):
@@ -131,7 +132,7 @@ struct Hit {
 __device__ __noinline__ Hit scan_linear(const SphereGeo* __restrict__ geo, uint32_t n, v3 o, v3 d,
                                         double tmin) {
   const double a = ykd::len2(d);
-  Hit h{INFINITY, -1, 0, 0};
+  Hit h{INFINITY, -1, 0, 0, 0, 0};
   for (uint32_t i = 0; i < n; ++i) {
     const SphereGeo sg = geo[i];
     ++h.tests;
@@ -141,7 +142,7 @@ __device__ __noinline__ Hit scan_linear(const SphereGeo* __restrict__ geo, uint3
     const double disc = hb * hb - a * c;
     if (disc < 0) continue;
     ++h.sqrts;
-    const double sq = ykd::nsqrt(disc);
+    const double sq = ykd::nsqrt_c(disc, h.ncalls, h.nits);
     double root = (-hb - sq) / a;
     if (root < tmin || h.T < root) {
       root = (-hb + sq) / a;
@@ -177,7 +178,7 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
   const double disc = hb * hb - a * c;
   if (disc < 0) return;  // never taken: the candidate passed the same test
   ++best.sqrts;
-  const double sq = ykd::nsqrt(disc);
+  const double sq = ykd::nsqrt_c(disc, best.ncalls, best.nits);
   double r = (-hb - sq) / a;
   if (r < tmin) {
     r = (-hb + sq) / a;
@@ -253,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
   g.a0 = g.a1 = g.b = g.j = g.seed = 0;
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
 
-  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0;
+  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0, n_ncall = 0, n_nit = 0;
 
 #if YK_ABLATE & 8
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
     //     sphere::hit_impl (sphere.hpp:25-48): tuple order, t_max shrinking to the last
     //     accepted root, so the closest hit wins and an exact tie goes to the later sphere.
     const bool alive = depth != 0;  // depth == 0 → black (raytracer.hpp:23)
-    Hit hit{INFINITY, -1, 0, 0};
+    Hit hit{INFINITY, -1, 0, 0, 0, 0};
     if (alive) {
       ++n_seg;
       const double a = ykd::len2(d);
@@ -436,6 +437,8 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         ++n_lin;
       }
       n_sqrt += hit.sqrts;
+      n_ncall += hit.ncalls;
+      n_nit += hit.nits;
     }
     YK_STAMP(3);
 
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         nrm = front ? outward : ykd::neg(outward);
         if (m.kind == YK_MATERIAL_LAMBERTIAN) vn = ykd::random_vec(g, -1, 1);  // vec3.hpp:134-142
       }
-      const double len = ykd::nsqrt(ykd::len2(vn));  // vec3::length(), vec3.hpp:127
+      const double len = ykd::nsqrt_c(ykd::len2(vn), n_ncall, n_nit);  // vec3::length(), vec3.hpp:127
       if (hid < 0) {
         // sky (raytracer.hpp:35-36): t = (normalized(dir).y + 1)/2, lerp white → (.5,.7,1)
         const double t = (d.y / len + 1.0) / 2;
@@ -482,7 +485,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
           nd = ykd::reflect(ykd::divs(d, len), nrm);
           if (m.fuzz > 0) {  // random_in_unit_sphere, material.hpp:27-30
             v3 ru = ykd::random_vec(g, -1, 1);
-            ru = ykd::divs(ru, ykd::nsqrt(ykd::len2(ru)));
+            ru = ykd::divs(ru, ykd::nsqrt_c(ykd::len2(ru), n_ncall, n_nit));
             const double k = ykd::uniform(g, 0.01, 0.99);
             nd = ykd::add(nd, ykd::mul(ykd::mul(ru, k), m.fuzz));
           }
@@ -493,14 +496,14 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
           const v3 unit = ykd::divs(d, len);
           double ct = ykd::dot(ykd::neg(unit), nrm);
           if (!(ct < 1.0)) ct = 1.0;
-          const double sn = ykd::nsqrt(1.0 - ct * ct);
+          const double sn = ykd::nsqrt_c(1.0 - ct * ct, n_ncall, n_nit);
           const bool cannot = ratio * sn > 1.0;
           if (cannot || ykd::reflectance(ct, ratio) > ykd::uniform(g, 0, 1)) {
             nd = ykd::reflect(unit, nrm);
           } else {
             const v3 perp = ykd::mul(ykd::add(unit, ykd::mul(nrm, ct)), ratio);
             const double pl = 1.0 - ykd::len2(perp);
-            nd = ykd::add(perp, ykd::mul(nrm, -ykd::nsqrt(pl < 0 ? -pl : pl)));
+            nd = ykd::add(perp, ykd::mul(nrm, -ykd::nsqrt_c(pl < 0 ? -pl : pl, n_ncall, n_nit)));
           }
         }
         if (!scattered) {
@@ -553,7 +556,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          double vq = ykd::nsqrt(q[c] / spp);
+          double vq = ykd::nsqrt_c(q[c] / spp, n_ncall, n_nit);
           vq = (vq < 0.0) ? 0.0 : (0.999 < vq) ? 0.999 : vq;
           ka.rgb[o3 + c] = (uint8_t)(uint32_t)(vq * 256);
         }
@@ -573,6 +576,8 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
     atomicAdd(&ka.counters[2], (unsigned long long)n_sqrt);
     atomicAdd(&ka.counters[4], (unsigned long long)n_node);
     atomicAdd(&ka.counters[5], (unsigned long long)n_lin);
+    atomicAdd(&ka.counters[6], (unsigned long long)n_ncall);
+    atomicAdd(&ka.counters[7], (unsigned long long)n_nit);
   }
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
@@ -756,6 +761,8 @@ int finish_stats(ykgpu_context* ctx) {
   YK_HIP(hipMemcpy(c, ctx->d_stats, sizeof(c), hipMemcpyDeviceToHost));
   ctx->stats.node_visits = c[4];
   ctx->stats.linear_scans = c[5];
+  ctx->stats.newton_calls = c[6];
+  ctx->stats.newton_iters = c[7];
   for (int k = 0; k < 6; ++k) ctx->stats.phase_cycles[k] = c[8 + k];
   ctx->stats.kernel_ms = ms;
   ctx->stats.segments = c[0];
@@ -870,7 +877,9 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   }
   double cam_ext = 0;
   for (int k = 0; k < 3; ++k) cam_ext = std::max(cam_ext, std::fabs(camera->origin[k]));
-  ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext);
+  ykbvh::Options bopt;
+  if (const char* e = std::getenv("YKGPU_BVH_LEAF")) bopt.max_leaf = std::max(1, std::min(15, std::atoi(e)));
+  ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, bopt);
   if (bvh.depth > ykbvh::kMaxDepth) return fail(YK_ERR_INVALID, "BVH deeper than the traversal stack");
   std::vector<SphereGeo> leaf_geo(count);
   for (uint32_t i = 0; i < count; ++i) leaf_geo[i] = geo[bvh.order[i]];

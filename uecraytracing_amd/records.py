@@ -93,6 +93,8 @@ class RenderStats(ctypes.Structure):
         ("mt_fallbacks", ctypes.c_uint64),
         ("node_visits", ctypes.c_uint64),
         ("linear_scans", ctypes.c_uint64),
+        ("newton_calls", ctypes.c_uint64),
+        ("newton_iters", ctypes.c_uint64),
         ("phase_cycles", ctypes.c_uint64 * 6),
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
