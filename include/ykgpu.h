@@ -151,6 +151,11 @@ int ykgpu_render_async(ykgpu_context* ctx, const yk_render_params* params, void*
  * pixel, row_count * W * 3 doubles, host buffer. */
 int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* params, double* sums_host);
 
+/* Diagnostics: the device's math::sqrt (math.hpp:10-19) -- the routine every length, root and
+ * to_color3b in the render uses -- on n host doubles (in and out may alias).  The tests check it
+ * against the reference's loop. */
+int ykgpu_math_sqrt(ykgpu_context* ctx, const double* in, double* out, uint64_t n);
+
 /* Statistics of the last render on this context. */
 int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out);
 

@@ -418,3 +418,9 @@ void yko_canonical_pattern(uint32_t seed, uint32_t count, double* out) {
 }
 
 double yko_newton_sqrt(double s) { return nsqrt(s); }
+
+/* Same over an array (the GPU test of ykgpu_math_sqrt).  Inputs must be finite and >= 0: the
+ * reference's loop never ends for NaN, inf or negative s. */
+void yko_newton_sqrt_n(const double* in, double* out, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) out[i] = nsqrt(in[i]);
+}

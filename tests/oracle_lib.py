@@ -41,6 +41,8 @@ def load():
     lib.yko_canonical_pattern.restype = None
     lib.yko_newton_sqrt.argtypes = [ctypes.c_double]
     lib.yko_newton_sqrt.restype = ctypes.c_double
+    lib.yko_newton_sqrt_n.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    lib.yko_newton_sqrt_n.restype = None
     _lib = lib
     return lib
 
@@ -90,3 +92,11 @@ def canonical_pattern(seed, count):
 
 def newton_sqrt(x):
     return load().yko_newton_sqrt(x)
+
+
+def newton_sqrt_array(values):
+    import numpy as np
+    a = np.ascontiguousarray(values, dtype=np.float64)
+    out = np.empty_like(a)
+    load().yko_newton_sqrt_n(a.ctypes.data, out.ctypes.data, a.size)
+    return out

@@ -44,6 +44,33 @@ def test_constexpr_build(ren):
     assert golden_data.sha(rgb) == MAN["constexpr_build"]["rgb_sha256"]
 
 
+def sqrt_inputs(rng, n_random=1 << 22):
+    """Doubles around every binade boundary (2^k +- m ulp) and at random exponents, all >= 0 and
+    finite (the reference's loop never ends otherwise), plus zero and the smallest subnormals."""
+    k = np.arange(-1074, 1024)
+    base = np.ldexp(1.0, k).view(np.int64)
+    m = np.arange(64)
+    near = np.concatenate([(base[:, None] + m).ravel(), (base[:, None] - m).ravel()]).view(np.float64)
+    near = near[np.isfinite(near) & (near >= 0)]
+    wide = np.ldexp(1.0 + rng.random(n_random), rng.integers(-1022, 1023, n_random))
+    unit = rng.random(n_random) * 4.0
+    kat = np.array([float.fromhex(a) for a, _ in golden_data.kat()["newton_sqrt"]])
+    return np.concatenate([[0.0, 5e-324, 1e-323, 2.2250738585072014e-308], near, wide, unit, kat])
+
+
+def test_math_sqrt_matches_reference_loop(ren):
+    """The device's math::sqrt starts at the IEEE sqrt (unique fixed point, DESIGN.md §3); it
+    must equal the reference's loop from s/2 bit for bit."""
+    x = sqrt_inputs(np.random.default_rng(11))
+    got = ren.math_sqrt(x)
+    want = oracle_lib.newton_sqrt_array(x)
+    bad = np.flatnonzero(got.view(np.int64) != want.view(np.int64))
+    assert bad.size == 0, [(x[i], got[i], want[i]) for i in bad[:5]]
+    kat = golden_data.kat()["newton_sqrt"]
+    got = ren.math_sqrt([float.fromhex(a) for a, _ in kat])
+    assert [g.hex() for g in got] == [float.fromhex(b).hex() for _, b in kat]
+
+
 EXT = [("rtiow5", 0, 80, 45, 16, 50), ("final", 42, 64, 36, 8, 50),
        ("glass", 42, 48, 27, 8, 200), ("final", 7, 40, 22, 12, 10)]
 

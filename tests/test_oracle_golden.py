@@ -28,6 +28,38 @@ def test_canonical_kat():
         assert [g.hex() for g in got] == [float.fromhex(v).hex() for v in vals], seed
 
 
+def _newton_from(s, x):
+    prev = 0.0
+    while x != prev:
+        prev, x = x, (x + s / x) / 2.0
+    return x
+
+
+def test_newton_sqrt_result_is_path_independent():
+    """The property the GPU's math::sqrt rests on (DESIGN.md §3): for normal s the reference loop
+    (math.hpp:10-19, from s/2) ends at the unique fixed point of x -> (x + s/x)/2, so starting
+    anywhere within a few ulps of sqrt(s) gives the same bits.  Python floats are IEEE doubles."""
+    import math
+    import random
+    rng = random.Random(5)
+    values = [math.ldexp(1.0 + rng.random(), rng.randrange(-1000, 1000)) for _ in range(20000)]
+    values += [rng.random() * 4.0 for _ in range(20000)]
+    for k in range(-1000, 1024, 3):  # both sides of every third binade boundary
+        b = math.ldexp(1.0, k)
+        up = down = b
+        for _ in range(8):
+            values += [up, down]
+            up, down = math.nextafter(up, math.inf), math.nextafter(down, 0.0)
+    for s in values:
+        if not math.isfinite(s):
+            continue
+        ref = oracle_lib.newton_sqrt(s)
+        r = math.sqrt(s)
+        for start in (r, math.nextafter(r, 0.0), math.nextafter(r, math.inf),
+                      math.nextafter(math.nextafter(r, math.inf), math.inf)):
+            assert _newton_from(s, start) == ref, (s.hex(), start.hex())
+
+
 def test_newton_sqrt_kat():
     for x, y in golden_data.kat()["newton_sqrt"]:
         assert oracle_lib.newton_sqrt(float.fromhex(x)).hex() == float.fromhex(y).hex(), x

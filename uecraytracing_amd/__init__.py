@@ -26,7 +26,7 @@ CLI_PATH = os.path.join(LIB_DIR, "raytrace")
 EXPORTS = (
     "ykgpu_abi_version", "ykgpu_last_error", "ykgpu_device_count", "ykgpu_context_create",
     "ykgpu_context_destroy", "ykgpu_set_scene", "ykgpu_render", "ykgpu_render_async",
-    "ykgpu_render_sums", "ykgpu_get_stats", "yk_camera_reference", "yk_camera_look",
+    "ykgpu_render_sums", "ykgpu_get_stats", "ykgpu_math_sqrt", "yk_camera_reference", "yk_camera_look",
     "yk_scene_build", "yk_image_height_for",
 )
 
@@ -66,6 +66,7 @@ def load_library():
         "ykgpu_render_async": ([c.c_void_p, P(RenderParams), c.c_void_p, c.c_void_p], c.c_int),
         "ykgpu_render_sums": ([c.c_void_p, P(RenderParams), c.c_void_p], c.c_int),
         "ykgpu_get_stats": ([c.c_void_p, P(RenderStats)], c.c_int),
+        "ykgpu_math_sqrt": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
         "yk_camera_reference": ([P(Camera)], c.c_int),
         "yk_camera_look": ([P(Camera), P(c.c_double), P(c.c_double), P(c.c_double), c.c_double,
                             c.c_double, c.c_double, c.c_double], c.c_int),
@@ -156,6 +157,13 @@ class Renderer:
         _check(self._lib.ykgpu_render_async(self._ctx, ctypes.byref(params),
                                             ctypes.c_void_p(rgb_device_ptr),
                                             ctypes.c_void_p(stream_ptr or None)))
+
+    def math_sqrt(self, values) -> np.ndarray:
+        """The device's math::sqrt (math.hpp:10-19) on a float64 array (diagnostic)."""
+        a = np.ascontiguousarray(values, dtype=np.float64)
+        out = np.empty_like(a)
+        _check(self._lib.ykgpu_math_sqrt(self._ctx, a.ctypes.data, out.ctypes.data, a.size))
+        return out
 
     def stats(self) -> dict:
         st = RenderStats()

@@ -26,20 +26,37 @@ __device__ __forceinline__ double dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y
 // length_squared(): vec3.hpp:129
 __device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
 
-// math::sqrt (math.hpp:10-19): Newton from s/2 until two iterates are equal.  Not IEEE sqrt
-// (differs by an ulp on ~25% of inputs), so it is replayed exactly.  The iteration bound only
-// matters for NaN/inf inputs (finite inputs converge in < 1100 steps; scene values in 5-17).
+// math::sqrt (math.hpp:10-19): x = s/2, then x = (x + s/x)/2 until two iterates are equal.
+// Not IEEE sqrt (differs by an ulp on ~25% of inputs), so its RESULT is reproduced exactly --
+// but not its path.  The loop can only stop at a fixed point of g(x) = fl(fl(x + fl(s/x))/2),
+// and for normal s that fixed point is UNIQUE: in units of ulp(x), x is fixed iff
+// RN(2(sqrt(s) - x)) is 0, or +-1 with x's significand even, which at most one double satisfies
+// ("math::sqrt").  So the same iteration started at the IEEE sqrt (within half an
+// ulp) ends at the reference's value after 1-2 steps instead of 5-17.  Checked against the
+// reference loop on every s = 2^k +- m ulp (k = -1074..1023, m < 2e5: 8.4e8 values) and 3e7
+// random values: only the smallest subnormal differs (s/2 underflows to 0), hence the guard
+// below, under which the reference start is kept.  YK_NEWTON_REF_START=1 restores the
+// reference start everywhere (A/B timing).  The iteration bound only matters for NaN/inf.
 // YK_ABLATE (timing-only builds, tools/ablate.py; results are WRONG by design):
 //   1 = skip the MT warm-up walk, 2 = hardware sqrt instead of math::sqrt
 #ifndef YK_ABLATE
 #define YK_ABLATE 0
 #endif
-
+#ifndef YK_NEWTON_REF_START
+#define YK_NEWTON_REF_START 0
+#endif
+__device__ __forceinline__ double nsqrt_start(double s) {
+#if YK_NEWTON_REF_START
+  return s / 2.0;
+#else
+  return (s >= 0x1p-1000 && s <= 0x1.fffffffffffffp+1023) ? __builtin_sqrt(s) : s / 2.0;
+#endif
+}
 __device__ __forceinline__ double nsqrt(double s) {
 #if YK_ABLATE & 2
   return sqrt(s);
 #endif
-  double x = s / 2.0, prev = 0.0;
+  double x = nsqrt_start(s), prev = 0.0;
   for (int guard = 0; x != prev && guard < 4096; ++guard) {
     prev = x;
     x = (x + s / x) / 2.0;
@@ -53,7 +70,7 @@ __device__ __forceinline__ double nsqrt_c(double s, uint32_t& calls, uint32_t& i
 #if YK_ABLATE & 2
   return sqrt(s);
 #endif
-  double x = s / 2.0, prev = 0.0;
+  double x = nsqrt_start(s), prev = 0.0;
   for (int guard = 0; x != prev && guard < 4096; ++guard) {
     prev = x;
     x = (x + s / x) / 2.0;

@@ -225,6 +225,13 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 // kSceneInLds: the BVH nodes, the leaf-ordered sphere geometry and the leaf→tuple ids are copied
 // into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
+
+// ykgpu_math_sqrt: the device's math::sqrt on a buffer (diagnostic entry point).
+__global__ __launch_bounds__(256) void yk_math_sqrt(const double* in, double* out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = ykd::nsqrt(in[i]);
+}
+
 template <bool kSceneInLds>
 __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -976,6 +983,25 @@ int ykgpu_render(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_hos
 int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* p, double* sums_host) {
   if (!sums_host) return fail(YK_ERR_INVALID, "null output");
   return render_host(ctx, p, nullptr, sums_host);
+}
+
+int ykgpu_math_sqrt(ykgpu_context* ctx, const double* in, double* out, uint64_t n) {
+  if (!ctx || (n && (!in || !out))) return fail(YK_ERR_INVALID, "null argument");
+  if (n == 0) return YK_OK;
+  YK_HIP(hipSetDevice(ctx->device));
+  double* d = nullptr;
+  YK_HIP(hipMalloc(&d, 2 * n * sizeof(double)));
+  hipError_t e = hipMemcpy(d, in, n * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(yk_math_sqrt, dim3((uint32_t)blocks), dim3(256), 0, ctx->stream, d, d + n, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, d + n, n * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_math_sqrt: ") + hipGetErrorString(e));
+  return YK_OK;
 }
 
 int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out) {
