@@ -18,7 +18,9 @@ r.render(p); ts = []
 for _ in range(3):
     r.render(p); ts.append(r.stats()["kernel_ms"])
 st = r.stats()
-print(json.dumps({"ms": min(ts), "segs": st["segments"] / st["samples"]}))
+sg = st["segments"]
+print(json.dumps({"ms": round(min(ts), 3), "segs": round(sg / st["samples"], 4),
+                  "nodes/seg": round(st["node_visits"] / sg, 3), "tests/seg": round(st["sphere_tests"] / sg, 3)}))
 ''' % ROOT
 variants = [("base", os.path.join(ROOT, "uecraytracing_amd/lib/libykgpu.so"))]
 for m in sys.argv[2:] or ["1", "2", "3"]:

@@ -26,6 +26,18 @@ struct alignas(16) Node {
 };
 static_assert(sizeof(Node) == 64, "Node layout");
 
+// Device layout of a Node (80 bytes), built by slab_nodes().  Per axis, both children's planes
+// as [lo pair][hi pair][lo pair]: a ray whose 1/d on that axis is >= 0 reads (near, far) =
+// (lo, hi) at byte 0 of the axis, a ray with 1/d < 0 reads (hi, lo) at byte 8 — one 16-byte
+// read per axis returns the planes already ordered, so the slab test needs no min/max
+// (rounding is monotonic, so the selection equals min/max of the two products).  child >= 0 is
+// the BYTE OFFSET of an inner node (no multiply per visit); leaves keep their negative codes.
+struct alignas(16) SlabNode {
+  float x[6], y[6], z[6];
+  int32_t child[2];
+};
+static_assert(sizeof(SlabNode) == 80, "SlabNode layout");
+
 struct Built {
   std::vector<Node> nodes;      // nodes[0] is the root when root >= 0
   std::vector<uint32_t> order;  // leaf slots → original sphere index (tuple order)
@@ -43,6 +55,9 @@ struct Options {
 // centers: 3 doubles per sphere; radii may be negative (hollow shells: |r| is used).
 Built build(const double* centers, const double* radii, uint32_t n, double camera_extent,
             const Options& opt = Options());
+// Nodes in SlabNode layout, and the root code in that encoding (byte offset or leaf code).
+std::vector<SlabNode> slab_nodes(const Built& b);
+int32_t slab_root(const Built& b);
 constexpr uint32_t kMaxDepth = 32;  // traversal stack capacity (device, LDS)
 
 }  // namespace ykbvh

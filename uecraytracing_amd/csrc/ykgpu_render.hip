@@ -105,7 +105,7 @@ struct KernelArgs {
   int32_t bvh_root;
   uint32_t n_nodes;
   uint32_t lds_geo_off, lds_ids_off, lds_stack_off, stack_depth;
-  const ykbvh::Node* __restrict__ nodes;
+  const ykbvh::SlabNode* __restrict__ nodes;  // child links are byte offsets from nodes
   const SphereGeo* __restrict__ leaf_geo;  // spheres in BVH leaf order
   const uint32_t* __restrict__ leaf_ids;   // leaf slot → tuple index
   const SphereGeo* __restrict__ geo;
@@ -153,6 +153,8 @@ __device__ __noinline__ Hit scan_linear(const SphereGeo* __restrict__ geo, uint3
   }
   return h;
 }
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float safe_rcp(float x) {
   return fabsf(x) > 1e-30f ? 1.0f / x : copysignf(1e30f, x);
@@ -237,20 +239,21 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const ykbvh::Node* __restrict__ nodes = ka.nodes;
+  const char* __restrict__ nodes = (const char*)ka.nodes;
   const SphereGeo* __restrict__ leaf_geo = ka.leaf_geo;
   const uint32_t* __restrict__ leaf_ids = ka.leaf_ids;
   if (kSceneInLds) {
     const uint4* src[3] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids};
     const uint32_t off[3] = {0u, ka.lds_geo_off, ka.lds_ids_off};
-    const uint32_t n16[3] = {ka.n_nodes * 4u, ka.nspheres * 2u, (ka.nspheres + 3u) / 4u};
+    const uint32_t n16[3] = {ka.n_nodes * (uint32_t)(sizeof(ykbvh::SlabNode) / 16), ka.nspheres * 2u,
+                             (ka.nspheres + 3u) / 4u};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       uint4* dst = (uint4*)(smem + off[k]);
       for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlock) dst[i] = src[k][i];
     }
     __syncthreads();
-    nodes = (const ykbvh::Node*)smem;
+    nodes = smem;
     leaf_geo = (const SphereGeo*)(smem + ka.lds_geo_off);
     leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
   }
@@ -344,6 +347,11 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         // arithmetic only, so explicit FMAs are fine here.
         const float ix = safe_rcp((float)d.x), iy = safe_rcp((float)d.y), iz = safe_rcp((float)d.z);
         const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
+        // byte offsets of this ray's (near, far) plane pairs inside a SlabNode (yk_bvh.hpp)
+        const uint32_t offx = ix < 0.0f ? 8u : 0u, offy = (iy < 0.0f ? 8u : 0u) + 24u,
+                       offz = (iz < 0.0f ? 8u : 0u) + 48u;
+        const f2 ixv = {ix, ix}, iyv = {iy, iy}, izv = {iz, iz};
+        const f2 noix = {-oix, -oix}, noiy = {-oiy, -oiy}, noiz = {-oiz, -oiz};
         const double ia = 1.0 / a;
         const float tminf = (float)ka.t_min;
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
@@ -354,17 +362,23 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         int32_t node = ka.bvh_root;
         uint32_t sp = 0;
         for (;;) {
-        if (node >= 0) {
+          if (node >= 0) {
             ++n_node;
-            const ykbvh::Node nd = nodes[node];
+            const char* nb = nodes + node;
+            // (near, far) planes of both children per axis, one packed FMA per pair:
+            // t = plane*(1/d) - o*(1/d)
+            const f2 nx = __builtin_elementwise_fma(*(const f2*)(nb + offx), ixv, noix);
+            const f2 fx = __builtin_elementwise_fma(*(const f2*)(nb + offx + 8), ixv, noix);
+            const f2 ny = __builtin_elementwise_fma(*(const f2*)(nb + offy), iyv, noiy);
+            const f2 fy = __builtin_elementwise_fma(*(const f2*)(nb + offy + 8), iyv, noiy);
+            const f2 nz = __builtin_elementwise_fma(*(const f2*)(nb + offz), izv, noiz);
+            const f2 fz = __builtin_elementwise_fma(*(const f2*)(nb + offz + 8), izv, noiz);
+            const int2 ch = *(const int2*)(nb + 72);
             float tn[2], tf[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-              const float ax = __builtin_fmaf(nd.lo_x[k], ix, -oix), bx = __builtin_fmaf(nd.hi_x[k], ix, -oix);
-              const float ay = __builtin_fmaf(nd.lo_y[k], iy, -oiy), by = __builtin_fmaf(nd.hi_y[k], iy, -oiy);
-              const float az = __builtin_fmaf(nd.lo_z[k], iz, -oiz), bz = __builtin_fmaf(nd.hi_z[k], iz, -oiz);
-              const float n0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-              const float f0 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+              const float n0 = fmaxf(fmaxf(nx[k], ny[k]), nz[k]);
+              const float f0 = fminf(fminf(fx[k], fy[k]), fz[k]);
               tn[k] = __builtin_fmaf(-fabsf(n0), 0x1p-20f, n0);  // relax by the error bound
               tf[k] = __builtin_fmaf(fabsf(f0), 0x1p-20f, f0);
             }
@@ -372,13 +386,13 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
             const bool h1 = tn[1] <= tf[1] && tf[1] >= tminf && tn[1] <= ustar_f;
             if (h0 && h1) {
               const bool first0 = tn[0] <= tn[1];
-              stk[sp * kBlock] = first0 ? nd.child[1] : nd.child[0];
+              stk[sp * kBlock] = first0 ? ch.y : ch.x;
               ++sp;
-              node = first0 ? nd.child[0] : nd.child[1];
+              node = first0 ? ch.x : ch.y;
               continue;
             }
             if (h0 || h1) {
-              node = h0 ? nd.child[0] : nd.child[1];
+              node = h0 ? ch.x : ch.y;
               continue;
             }
           } else {
@@ -613,7 +627,7 @@ struct ykgpu_context {
   bool have_scene = false;
   uint32_t* d_counter = nullptr;        // [0] pixel counter
   unsigned long long* d_stats = nullptr;  // kCounters counters
-  ykbvh::Node* d_nodes = nullptr;
+  ykbvh::SlabNode* d_nodes = nullptr;
   SphereGeo* d_leaf_geo = nullptr;
   uint32_t* d_leaf_ids = nullptr;
   int32_t bvh_root = 0;
@@ -896,26 +910,27 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   ctx->d_nodes = nullptr;
   ctx->d_leaf_geo = nullptr;
   ctx->d_leaf_ids = nullptr;
-  const size_t nn = std::max<size_t>(1, bvh.nodes.size());
-  YK_HIP(hipMalloc(&ctx->d_nodes, nn * sizeof(ykbvh::Node)));
+  const std::vector<ykbvh::SlabNode> snodes = ykbvh::slab_nodes(bvh);
+  const size_t nn = std::max<size_t>(1, snodes.size());
+  YK_HIP(hipMalloc(&ctx->d_nodes, nn * sizeof(ykbvh::SlabNode)));
   YK_HIP(hipMalloc(&ctx->d_leaf_geo, count * sizeof(SphereGeo)));
   YK_HIP(hipMalloc(&ctx->d_leaf_ids, count * sizeof(uint32_t)));
-  if (!bvh.nodes.empty())
-    YK_HIP(hipMemcpy(ctx->d_nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(ykbvh::Node),
+  if (!snodes.empty())
+    YK_HIP(hipMemcpy(ctx->d_nodes, snodes.data(), snodes.size() * sizeof(ykbvh::SlabNode),
                      hipMemcpyHostToDevice));
   YK_HIP(hipMemcpy(ctx->d_leaf_geo, leaf_geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
   YK_HIP(hipMemcpy(ctx->d_leaf_ids, bvh.order.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
-  ctx->bvh_root = bvh.root;
+  ctx->bvh_root = ykbvh::slab_root(bvh);
   ctx->bvh_depth = bvh.depth;
   ctx->origin_bound = bvh.origin_bound;
   ctx->n_nodes = (uint32_t)bvh.nodes.size();
   // LDS layout: [nodes][leaf geometry][leaf ids][traversal stacks]
   auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  const size_t scene_bytes = a16(ctx->n_nodes * sizeof(ykbvh::Node)) + a16(count * sizeof(SphereGeo)) +
+  const size_t scene_bytes = a16(ctx->n_nodes * sizeof(ykbvh::SlabNode)) + a16(count * sizeof(SphereGeo)) +
                              a16(count * sizeof(uint32_t));
   ctx->scene_in_lds = scene_bytes <= 64 * 1024;
   ctx->stack_depth = bvh.depth + 1;
-  ctx->lds_geo_off = (uint32_t)a16(ctx->n_nodes * sizeof(ykbvh::Node));
+  ctx->lds_geo_off = (uint32_t)a16(ctx->n_nodes * sizeof(ykbvh::SlabNode));
   ctx->lds_ids_off = ctx->lds_geo_off + (uint32_t)a16(count * sizeof(SphereGeo));
   ctx->lds_stack_off = ctx->scene_in_lds ? (uint32_t)scene_bytes : 0u;
   ctx->lds_bytes = ctx->lds_stack_off + ctx->stack_depth * kBlock * (uint32_t)sizeof(int32_t);
