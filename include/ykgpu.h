@@ -156,6 +156,11 @@ int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* params, double
  * against the reference's loop. */
 int ykgpu_math_sqrt(ykgpu_context* ctx, const double* in, double* out, uint64_t n);
 
+/* Diagnostics: the renderer's vector / scalar division (the normalisations and normals of
+ * sphere.hpp / vec3.hpp) on n host triples: out3[3i+k] = num3[3i+k] / den[i].  It must equal
+ * IEEE division bit for bit; the tests check it. */
+int ykgpu_math_div(ykgpu_context* ctx, const double* num3, const double* den, double* out3, uint64_t n);
+
 /* Statistics of the last render on this context. */
 int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out);
 

@@ -71,6 +71,39 @@ def test_math_sqrt_matches_reference_loop(ren):
     assert [g.hex() for g in got] == [float.fromhex(b).hex() for _, b in kat]
 
 
+def test_fast_division_is_ieee_division(ren):
+    """The renderer's vector / scalar division skips div_scale / div_fixup for operands in
+    [2^-400, 2^400] (yk_device.hpp); it must be IEEE division bit for bit everywhere: random
+    operands of every sign and exponent, both sides of the range edges, zeros of both signs,
+    subnormals and infinities (those take the full-division fallback)."""
+    rng = np.random.default_rng(3)
+    n = 1 << 21
+
+    def draw(size, lo, hi):
+        v = np.ldexp(1.0 + rng.random(size), rng.integers(lo, hi, size))
+        return np.where(rng.random(size) < 0.5, -v, v)
+
+    num = draw((n, 3), -420, 420)
+    den = draw(n, -420, 420)
+    num[: n // 8] = draw((n // 8, 3), -4, 4)          # the renderer's magnitudes
+    den[: n // 8] = draw(n // 8, -2, 4)
+    lo, hi = np.ldexp(1.0, -400), np.ldexp(1.0, 400)
+    edges = np.array([lo, hi, np.nextafter(lo, 0), np.nextafter(hi, np.inf)])
+    k = np.arange(4096)
+    num[n // 8:n // 8 + 4096] = edges[k % 4, None] * np.array([1.0, -1.0, 3.0])
+    den[n // 8:n // 8 + 4096] = edges[(k // 4) % 4] * np.where(k % 3 == 0, -1.0, 1.0)
+    special = np.array([0.0, -0.0, 5e-324, -5e-324, np.inf, -np.inf, 1.0, -2.5])
+    m = n // 4
+    num[m:m + 512] = special[rng.integers(0, 8, (512, 3))]
+    den[m:m + 512] = special[rng.integers(4, 8, 512)]
+    got = ren.math_div(num, den)
+    with np.errstate(all="ignore"):
+        want = num / den[:, None]
+    same = (got.view(np.int64) == want.view(np.int64)) | (np.isnan(got) & np.isnan(want))
+    bad = np.argwhere(~same)
+    assert bad.size == 0, [(num[i, j], den[i], got[i, j], want[i, j]) for i, j in bad[:5]]
+
+
 EXT = [("rtiow5", 0, 80, 45, 16, 50), ("final", 42, 64, 36, 8, 50),
        ("glass", 42, 48, 27, 8, 200), ("final", 7, 40, 22, 12, 10)]
 

@@ -1,0 +1,237 @@
+// tools/ubench.hip — issue cost of single VALU instructions / short sequences on gfx950: one
+// wave per SIMD, eight independent chains, clock64() around the loop.  Diagnostic only: says
+// which FP64 / integer operations the render loop should avoid.
+//   build: hipcc -O3 --offload-arch=gfx950 -o tools/ubench tools/ubench.hip ; run: tools/ubench
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cmath>
+#include <cstdio>
+
+constexpr int kChains = 8;
+constexpr int kIters = 2048;
+
+struct FmaF32 {
+  using T = float;
+  static __device__ void op(T& x, T a, T b) { asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x) : "v"(a), "v"(b)); }
+};
+struct PkFmaF32 {
+  using T = double;  // two packed floats in a 64-bit register pair
+  static __device__ void op(T& x, T a, T b) { asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(x) : "v"(a), "v"(b)); }
+};
+struct FmaF64 {
+  using T = double;
+  static __device__ void op(T& x, T a, T b) { asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(x) : "v"(a), "v"(b)); }
+};
+struct MulF64 {
+  using T = double;
+  static __device__ void op(T& x, T a, T) { asm volatile("v_mul_f64 %0, %1, %0" : "+v"(x) : "v"(a)); }
+};
+struct AddF64 {
+  using T = double;
+  static __device__ void op(T& x, T a, T) { asm volatile("v_add_f64 %0, %1, %0" : "+v"(x) : "v"(a)); }
+};
+struct RcpF64 {
+  using T = double;
+  static __device__ void op(T& x, T, T) { asm volatile("v_rcp_f64 %0, %0" : "+v"(x)); }
+};
+struct RsqF64 {
+  using T = double;
+  static __device__ void op(T& x, T, T) { asm volatile("v_rsq_f64 %0, %0" : "+v"(x)); }
+};
+struct SqrtF64 {
+  using T = double;
+  static __device__ void op(T& x, T, T) { asm volatile("v_sqrt_f64 %0, %0" : "+v"(x)); }
+};
+struct RcpF32 {
+  using T = float;
+  static __device__ void op(T& x, T, T) { asm volatile("v_rcp_f32 %0, %0" : "+v"(x)); }
+};
+struct MinMax3F32 {
+  using T = float;
+  static __device__ void op(T& x, T a, T b) { asm volatile("v_max3_f32 %0, %1, %2, %0" : "+v"(x) : "v"(a), "v"(b)); }
+};
+struct CmpF64 {  // compare + select, the shape of the culling tests (compiler generated)
+  using T = double;
+  static __device__ void op(T& x, T a, T b) { x = (x < a) ? b : x + b; asm volatile("" : "+v"(x)); }
+};
+struct MulLoU32 {
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T) { asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(x) : "v"(a)); }
+};
+struct XorShrU32 {  // x ^ (x >> 30): the seeding step's shift-xor
+  using T = uint32_t;
+  static __device__ void op(T& x, T, T) {
+    uint32_t t;
+    asm volatile("v_lshrrev_b32 %1, 30, %0\n\tv_xor_b32 %0, %0, %1" : "+v"(x), "=&v"(t));
+  }
+};
+struct CmpLtF64 {  // v_cmp into an SGPR pair, then used by a cndmask so it is not dead
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T b) {
+    const double da = (double)a, db = (double)b;
+    asm volatile("v_cmp_lt_f64_e64 s[40:41], %1, %2\n\tv_cndmask_b32_e64 %0, %0, 1, s[40:41]" : "+v"(x) : "v"(da), "v"(db) : "s40", "s41");
+  }
+};
+struct CmpClassF64 {
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T) {
+    const double da = (double)a;
+    const uint32_t m = 0x60u;
+    asm volatile("v_cmp_class_f64_e64 s[40:41], %1, %2\n\tv_cndmask_b32_e64 %0, %0, 1, s[40:41]" : "+v"(x) : "v"(da), "v"(m) : "s40", "s41");
+  }
+};
+struct CmpLtU32 {
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T) {
+    asm volatile("v_cmp_lt_u32_e64 s[40:41], %0, %1\n\tv_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(x) : "v"(a) : "s40", "s41");
+  }
+};
+struct CndOnly {
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T) {
+    asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(x) : "v"(a) : "s40", "s41");
+  }
+};
+struct DivScaleF64 {
+  using T = double;
+  static __device__ void op(T& x, T a, T) { asm volatile("v_div_scale_f64 %0, vcc, %0, %1, %0" : "+v"(x) : "v"(a) : "vcc"); }
+};
+struct DivFixupF64 {
+  using T = double;
+  static __device__ void op(T& x, T a, T b) { asm volatile("v_div_fixup_f64 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b)); }
+};
+struct DivFmasF64 {
+  using T = double;
+  static __device__ void op(T& x, T a, T b) { asm volatile("s_mov_b64 vcc, 0\n\tv_div_fmas_f64 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b) : "vcc"); }
+};
+struct BfeU32 {
+  using T = uint32_t;
+  static __device__ void op(T& x, T, T) { asm volatile("v_bfe_u32 %0, %0, 20, 11" : "+v"(x)); }
+};
+// whole sequences, compiler generated (not asm): correctly rounded division and sqrt
+struct DivF64 {
+  using T = double;
+  static __device__ void op(T& x, T a, T) { x = a / x; asm volatile("" : "+v"(x)); }
+};
+struct SqrtLibF64 {
+  using T = double;
+  static __device__ void op(T& x, T, T) { x = __builtin_sqrt(x); asm volatile("" : "+v"(x)); }
+};
+
+template <class Op>
+__global__ __launch_bounds__(64) void bench(uint64_t* cyc, typename Op::T* sink, typename Op::T a,
+                                            typename Op::T b, typename Op::T init) {
+  using T = typename Op::T;
+  T x[kChains];
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) x[k] = init;
+  const uint64_t t0 = clock64();
+  for (int i = 0; i < kIters; ++i) {
+#pragma unroll
+    for (int k = 0; k < kChains; ++k) Op::op(x[k], a, b);
+  }
+  const uint64_t t1 = clock64();
+  T s = x[0];
+#pragma unroll
+  for (int k = 1; k < kChains; ++k) s = s + x[k];
+  sink[blockIdx.x * 64 + threadIdx.x] = s;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <class Op>
+void run(const char* name, typename Op::T a, typename Op::T b, typename Op::T init, int waves) {
+  using T = typename Op::T;
+  uint64_t* cyc;
+  T* sink;
+  (void)hipMalloc(&cyc, waves * sizeof(uint64_t));
+  (void)hipMalloc(&sink, waves * 64 * sizeof(T));
+  hipLaunchKernelGGL(bench<Op>, dim3(waves), dim3(64), 0, 0, cyc, sink, a, b, init);
+  hipLaunchKernelGGL(bench<Op>, dim3(waves), dim3(64), 0, 0, cyc, sink, a, b, init);
+  (void)hipDeviceSynchronize();
+  uint64_t h[4096];
+  (void)hipMemcpy(h, cyc, waves * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  double mean = 0;
+  for (int i = 0; i < waves; ++i) mean += (double)h[i];
+  mean /= waves;
+  printf("%-12s waves=%5d  %.2f clock64 ticks per op per wave\n", name, waves, mean / ((double)kIters * kChains));
+  (void)hipFree(cyc);
+  (void)hipFree(sink);
+}
+
+// accuracy of the hardware approximations (max error in units of 2^-52 relative)
+__global__ void approx(const double* in, double* out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x = in[i], r, s, q;
+  asm volatile("v_rsq_f64 %0, %1" : "=v"(r) : "v"(x));
+  asm volatile("v_sqrt_f64 %0, %1" : "=v"(s) : "v"(x));
+  asm volatile("v_rcp_f64 %0, %1" : "=v"(q) : "v"(x));
+  out[3 * i] = r;
+  out[3 * i + 1] = s;
+  out[3 * i + 2] = q;
+}
+
+void accuracy() {
+  const uint64_t n = 1 << 22;
+  double* h = new double[n];
+  double* o = new double[3 * n];
+  uint64_t st = 88172645463325252ull;
+  for (uint64_t i = 0; i < n; ++i) {
+    st ^= st << 13, st ^= st >> 7, st ^= st << 17;
+    const double m = 1.0 + (double)(st >> 11) * 0x1p-53;
+    const int e = (int)((st >> 3) % 1200) - 600;
+    h[i] = __builtin_ldexp(m, e);
+  }
+  double *d_in, *d_out;
+  (void)hipMalloc(&d_in, n * 8);
+  (void)hipMalloc(&d_out, 3 * n * 8);
+  (void)hipMemcpy(d_in, h, n * 8, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(approx, dim3((n + 255) / 256), dim3(256), 0, 0, d_in, d_out, n);
+  (void)hipMemcpy(o, d_out, 3 * n * 8, hipMemcpyDeviceToHost);
+  long double worst[3] = {0, 0, 0};
+  for (uint64_t i = 0; i < n; ++i) {
+    const long double x = h[i], sq = sqrtl(x);
+    const long double ref[3] = {1.0L / sq, sq, 1.0L / x};
+    for (int k = 0; k < 3; ++k) {
+      long double e = ((long double)o[3 * i + k] - ref[k]) / ref[k];
+      if (e < 0) e = -e;
+      if (e > worst[k]) worst[k] = e;
+    }
+  }
+  printf("max relative error / 2^-52:  rsq %.3Lg   sqrt %.3Lg   rcp %.3Lg\n", worst[0] * 0x1p52L,
+         worst[1] * 0x1p52L, worst[2] * 0x1p52L);
+}
+
+int main() {
+  accuracy();
+  hipDeviceProp_t p;
+  (void)hipGetDeviceProperties(&p, 0);
+  printf("%s  CUs %d  clock %d kHz\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
+  for (int waves : {p.multiProcessorCount * 4, p.multiProcessorCount * 8}) {
+    run<FmaF32>("fma_f32", 1.0000001f, 0.5f, 1.0f, waves);
+    run<PkFmaF32>("pk_fma_f32", 1.0, 0.5, 1.0, waves);
+    run<MinMax3F32>("max3_f32", 1.0f, 0.5f, 1.0f, waves);
+    run<RcpF32>("rcp_f32", 0, 0, 1.5f, waves);
+    run<FmaF64>("fma_f64", 1.0000001, 0.5, 1.0, waves);
+    run<MulF64>("mul_f64", 1.0000001, 0, 1.0, waves);
+    run<AddF64>("add_f64", 1e-9, 0, 1.0, waves);
+    run<CmpF64>("cmp+add_f64", 2.0, 1e-9, 1.0, waves);
+    run<RcpF64>("rcp_f64", 0, 0, 1.5, waves);
+    run<RsqF64>("rsq_f64", 0, 0, 1.5, waves);
+    run<SqrtF64>("v_sqrt_f64", 0, 0, 1.5, waves);
+    run<DivF64>("div_f64 seq", 1.5, 0, 1.2, waves);
+    run<SqrtLibF64>("sqrt_f64 seq", 0, 0, 1.5, waves);
+    run<MulLoU32>("mul_lo_u32", 1812433253u, 0, 7u, waves);
+    run<CmpLtF64>("cmp_f64+cnd", 2u, 3u, 1u, waves);
+    run<CmpClassF64>("cls_f64+cnd", 2u, 0, 1u, waves);
+    run<CmpLtU32>("cmp_u32+cnd", 5u, 0, 7u, waves);
+    run<CndOnly>("cndmask", 5u, 0, 7u, waves);
+    run<DivScaleF64>("div_scale", 1.5, 0, 1.25, waves);
+    run<DivFixupF64>("div_fixup", 1.5, 1.25, 1.2, waves);
+    run<DivFmasF64>("div_fmas", 1.0000001, 1e-9, 1.0, waves);
+    run<BfeU32>("bfe_u32", 0, 0, 0x3ff00000u, waves);
+    run<XorShrU32>("xor_shr_u32", 0, 0, 7u, waves);
+  }
+  return 0;
+}

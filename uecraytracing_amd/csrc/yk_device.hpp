@@ -45,23 +45,125 @@ __device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.
 #ifndef YK_NEWTON_REF_START
 #define YK_NEWTON_REF_START 0
 #endif
-__device__ __forceinline__ double nsqrt_start(double s) {
-#if YK_NEWTON_REF_START
-  return s / 2.0;
-#else
-  return (s >= 0x1p-1000 && s <= 0x1.fffffffffffffp+1023) ? __builtin_sqrt(s) : s / 2.0;
+// ---- division and square roots without the special-case steps ------------------------------
+// A correctly rounded double division on gfx950 is the compiler's sequence
+//   div_scale(d), div_scale(n), rcp, 4 fma (reciprocal refinement), mul, fma (residual),
+//   div_fmas, div_fixup                          (measured 49 cycles/SIMD per wave, tools/ubench)
+// div_scale only rescales operands at the extremes of the exponent range, div_fmas is a plain
+// fma when nothing was scaled, and div_fixup only rewrites NaN/inf/zero/denormal cases.  For
+// operands in [2^-400, 2^400] (or a zero numerator) the sequence below is therefore the same
+// arithmetic, operation for operation, minus those steps -- and the refined reciprocal depends
+// only on the divisor, so it is computed once for a vector / scalar.  Bit-identical to `/`:
+// checked by tests/test_gpu_parity.py::test_fast_division_is_ieee_division (ykgpu_math_div).
+#ifndef YK_DIVFAST
+#define YK_DIVFAST 1
 #endif
+#ifndef YK_BOUNDAPPROX
+#define YK_BOUNDAPPROX 1
+#endif
+#ifndef YK_NEWTONFAST
+#define YK_NEWTONFAST 1
+#endif
+__device__ __forceinline__ bool div_range(double x) { return fabs(x) >= 0x1p-400 && fabs(x) <= 0x1p400; }
+__device__ __forceinline__ bool num_range(double x) { return x == 0.0 || div_range(x); }
+__device__ __forceinline__ double rcp_refined(double s) {
+  const double r0 = __builtin_amdgcn_rcp(s);
+  double t = __builtin_fma(-s, r0, 1.0);
+  const double r1 = __builtin_fma(r0, t, r0);
+  t = __builtin_fma(-s, r1, 1.0);
+  return __builtin_fma(r1, t, r1);
+}
+// n / s given r = rcp_refined(s), both in range.  A zero numerator's quotient is q0 = n * r with
+// the IEEE sign; the final fma would turn -0 into +0, and for n != 0 q and q0 share their sign,
+// so copysign(q, q0) is exact in both cases (one v_bfi).
+__device__ __forceinline__ double div_by(double n, double s, double r) {
+  const double q0 = n * r;
+  const double e = __builtin_fma(-s, q0, n);
+  return __builtin_copysign(__builtin_fma(e, r, q0), q0);
+}
+// Same for n > 0 (math::sqrt's s / x).
+__device__ __forceinline__ double div_pos(double n, double s, double r) {
+  const double q0 = n * r;
+  return __builtin_fma(__builtin_fma(-s, q0, n), r, q0);
+}
+// vector / scalar: fast quotients for every lane; if any lane of the wave has an operand outside
+// the range, the whole wave recomputes with the full division (same bits for in-range lanes), so
+// there is no per-lane branch nest.
+__device__ __forceinline__ v3 divs_fast(v3 a, double s) {
+  if (!YK_DIVFAST) return divs(a, s);
+  const double r = rcp_refined(s);
+  v3 q = {div_by(a.x, s, r), div_by(a.y, s, r), div_by(a.z, s, r)};
+  const bool ok = div_range(s) && num_range(a.x) && num_range(a.y) && num_range(a.z);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) q = divs(a, s);
+  return q;
+}
+// n / d for n >= 0 and a small integer d with y = RN(1/d) from the host: Markstein's theorem
+// (y correctly rounded, q0 = RN(n*y) within an ulp => fma(fma(-d, q0, n), y, q0) = RN(n/d)).
+__device__ __forceinline__ double div_markstein(double n, double d, double y) {
+  if (!YK_DIVFAST) return n / d;
+  const double q0 = n * y;
+  return __builtin_fma(__builtin_fma(-d, q0, n), y, q0);
+}
+
+// Bounds-only approximations (the BVH's root bounds; never a result):
+// v_rsq_f64 / v_rcp_f64 are within 2^-23 (ISA: 2^29 ulp; measured 2^-24.2), one Newton step
+// squares that: relative error < 2^-44.
+__device__ __forceinline__ double sqrt_bound(double x) {  // x >= 0
+  if (!YK_BOUNDAPPROX) return __builtin_sqrt(x);
+  const double r = __builtin_amdgcn_rsq(x);
+  const double y = x * r, h = 0.5 * r;
+  const double y1 = __builtin_fma(__builtin_fma(-y, y, x), h, y);
+  return x == 0.0 ? 0.0 : y1;
+}
+__device__ __forceinline__ double rcp_bound(double a) {  // a > 0
+  if (!YK_BOUNDAPPROX) return 1.0 / a;
+  const double r0 = __builtin_amdgcn_rcp(a);
+  return __builtin_fma(r0, __builtin_fma(-a, r0, 1.0), r0);
+}
+// Start of math::sqrt's loop (any start gives the same fixed point; this one is the library's
+// correctly rounded sqrt without its denormal rescaling, valid for s in [2^-400, 2^400]).
+__device__ __forceinline__ double sqrt_start(double s) {
+  const double r = __builtin_amdgcn_rsq(s);
+  double g = s * r, h = r * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-g, g, s);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, s);
+  return __builtin_fma(d, h, g);
+}
+
+__device__ __forceinline__ double nsqrt_impl(double s, uint32_t& iters) {
+  double x, prev = 0.0;
+#if !YK_NEWTON_REF_START
+  if (YK_NEWTONFAST && s >= 0x1p-400 && s <= 0x1p400) {
+    // iterates stay within [2^-201, 2^201]: the division needs no special-case steps
+    x = sqrt_start(s);
+    for (int guard = 0; x != prev && guard < 4096; ++guard) {
+      prev = x;
+      x = (x + div_pos(s, x, rcp_refined(x))) / 2.0;
+      ++iters;
+    }
+    return x;
+  }
+  x = (s >= 0x1p-1000 && s <= 0x1.fffffffffffffp+1023) ? __builtin_sqrt(s) : s / 2.0;
+#else
+  x = s / 2.0;
+#endif
+  for (int guard = 0; x != prev && guard < 4096; ++guard) {
+    prev = x;
+    x = (x + s / x) / 2.0;
+    ++iters;
+  }
+  return x;
 }
 __device__ __forceinline__ double nsqrt(double s) {
 #if YK_ABLATE & 2
   return sqrt(s);
 #endif
-  double x = nsqrt_start(s), prev = 0.0;
-  for (int guard = 0; x != prev && guard < 4096; ++guard) {
-    prev = x;
-    x = (x + s / x) / 2.0;
-  }
-  return x;
+  uint32_t it = 0;
+  return nsqrt_impl(s, it);
 }
 
 // Same, counting calls and loop iterations (work counters of the roofline model).
@@ -70,13 +172,7 @@ __device__ __forceinline__ double nsqrt_c(double s, uint32_t& calls, uint32_t& i
 #if YK_ABLATE & 2
   return sqrt(s);
 #endif
-  double x = nsqrt_start(s), prev = 0.0;
-  for (int guard = 0; x != prev && guard < 4096; ++guard) {
-    prev = x;
-    x = (x + s / x) / 2.0;
-    ++iters;
-  }
-  return x;
+  return nsqrt_impl(s, iters);
 }
 
 __device__ __forceinline__ v3 normalized(v3 a) { return divs(a, nsqrt(len2(a))); }  // :127,132

@@ -69,7 +69,13 @@ struct alignas(16) SphereMat {
 };
 static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 
-constexpr int kBlock = 256;
+#ifndef YK_BLOCK
+#define YK_BLOCK 256
+#endif
+#ifndef YK_WAVES_PER_EU
+#define YK_WAVES_PER_EU 0
+#endif
+constexpr int kBlock = YK_BLOCK;
 constexpr int kCounters = 16;
 
 // Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
@@ -101,6 +107,7 @@ struct KernelArgs {
   uint32_t pix_base, pad1;          // this launch renders tile pixels [pix_base, pix_base + npix)
   const uint32_t* __restrict__ warm;  // x_397 per sample of the launch, [(pix - pix_base)*spp + s]
   double t_min;
+  double inv_w, inv_h;  // RN(1/W), RN(1/H) for the camera's exact divisions (div_markstein)
   double origin_bound;  // |o|_inf beyond which the BVH's float culling is not proven sound
   int32_t bvh_root;
   uint32_t n_nodes;
@@ -171,8 +178,17 @@ __device__ __forceinline__ float safe_rcp(float x) {
 
 // Exact value of sphere i's root under the reference's acceptance rule, ignoring t_max
 // (sphere.hpp:35-39): root1 if root1 >= t_min, else root2 if root2 >= t_min, else none.
+// n / a for a root (sphere.hpp:36-38), a's refined reciprocal shared by all candidates; a wave
+// with any lane out of range takes the full division (divs_fast's rule)
+__device__ __forceinline__ double root_div(double n, double a, double ra, bool a_ok) {
+  if (!YK_DIVFAST) return n / a;
+  double q = ykd::div_by(n, a, ra);
+  if (__builtin_expect(__ballot(!(a_ok && ykd::num_range(n))) != 0, 0)) q = n / a;
+  return q;
+}
 __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ geo, uint32_t i,
-                                                v3 o, v3 d, double a, double tmin, Hit& best) {
+                                                v3 o, v3 d, double a, double ra, bool a_ok,
+                                                double tmin, Hit& best) {
   const SphereGeo sg = geo[i];
   const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
   const double hb = ykd::dot(oc, d);
@@ -181,9 +197,9 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
   if (disc < 0) return;  // never taken: the candidate passed the same test
   ++best.sqrts;
   const double sq = ykd::nsqrt_c(disc, best.ncalls, best.nits);
-  double r = (-hb - sq) / a;
+  double r = root_div(-hb - sq, a, ra, a_ok);
   if (r < tmin) {
-    r = (-hb + sq) / a;
+    r = root_div(-hb + sq, a, ra, a_ok);
     if (r < tmin) return;
   }
   // closest wins; an exact tie goes to the later tuple index (hittable_list.hpp:36-43)
@@ -228,14 +244,31 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 // into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
 
+// ykgpu_math_div: the renderer's vector / scalar division (divs_fast) on a buffer (diagnostic).
+__global__ __launch_bounds__(256) void yk_math_div(const double* num3, const double* den, double* out3,
+                                                  uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ykd::v3 q = ykd::divs_fast({num3[3 * i], num3[3 * i + 1], num3[3 * i + 2]}, den[i]);
+  out3[3 * i] = q.x;
+  out3[3 * i + 1] = q.y;
+  out3[3 * i + 2] = q.z;
+}
+
 // ykgpu_math_sqrt: the device's math::sqrt on a buffer (diagnostic entry point).
 __global__ __launch_bounds__(256) void yk_math_sqrt(const double* in, double* out, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = ykd::nsqrt(in[i]);
 }
 
-template <bool kSceneInLds>
-__global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
+// kCount: the work counters of YK_FLAG_COUNT_WORK (an instance of its own, so the production
+// instance carries neither their registers nor their adds)
+template <bool kSceneInLds, bool kCount>
+__global__ __launch_bounds__(kBlock)
+#if YK_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
+#endif
+void yk_render_persistent(KernelArgs ka) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -301,8 +334,9 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
       // seed (uint32 wrap, source.cpp:154-158); x_397 comes from yk_mt_warmup
       ykd::mt_start_from(g, ka.seed0 + (y * ka.W + x) * ka.spp + s,
                          ka.warm[(size_t)(pix - ka.pix_base) * ka.spp + s]);
-      const double u = ((double)x + ykd::uniform(g, 0, 1)) / (double)ka.W;
-      const double v = ((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1)) / (double)ka.H;
+      // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
+      const double u = ykd::div_markstein((double)x + ykd::uniform(g, 0, 1), (double)ka.W, ka.inv_w);
+      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1), (double)ka.H, ka.inv_h);
       // camera::get_ray (camera.hpp:29-32): llc + u*horizontal + v*vertical (- origin)
       const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
       const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
@@ -352,12 +386,14 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
                        offz = (iz < 0.0f ? 8u : 0u) + 48u;
         const f2 ixv = {ix, ix}, iyv = {iy, iy}, izv = {iz, iz};
         const f2 noix = {-oix, -oix}, noiy = {-oiy, -oiy}, noiz = {-oiz, -oiz};
-        const double ia = 1.0 / a;
+        const double ia = ykd::rcp_bound(a);  // bounds only: relative error < 2^-44
         const float tminf = (float)ka.t_min;
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
         float ustar_f = INFINITY;
         uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-        double l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+        // candidate lower bounds kept as floats rounded down, compared with ustar_f (>= U*):
+        // both only ever keep MORE candidates than the double comparison would
+        float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
         bool overflow = false;
         int32_t node = ka.bvh_root;
         uint32_t sp = 0;
@@ -406,10 +442,10 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
               const double c = ykd::len2(oc) - sg.rr;
               const double disc = hb * hb - a * c;
               if (disc < 0) continue;
-              // bounds of the exact root: |approx - exact| <= m (500x the rounding bound)
-              const double sq = sqrt(disc);
+              // bounds of the exact root: |approx - exact| <= m (256x the error bound, §4)
+              const double sq = ykd::sqrt_bound(disc);
               const double r1 = (-hb - sq) * ia, r2 = (-hb + sq) * ia;
-              const double m = (fabs(hb) + sq) * ia * 0x1p-40 + 0x1p-1000;
+              const double m = (fabs(hb) + sq) * ia * 0x1p-34 + 0x1p-1000;
               if (r2 + m < ka.t_min) continue;  // both roots certainly behind t_min
               const double lb = fmax(ka.t_min, r1 - m);
               const double ub = (r1 - m >= ka.t_min) ? r1 + m : ((r2 - m >= ka.t_min) ? r2 + m : INFINITY);
@@ -422,15 +458,15 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
                 uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
-                double e0 = l0, e1 = l1, e2 = l2, e3 = l3;
-                if (e0 <= ustar) { YK_CAND_SET(m2, d0, e0); ++m2; }
-                if (e1 <= ustar) { YK_CAND_SET(m2, d1, e1); ++m2; }
-                if (e2 <= ustar) { YK_CAND_SET(m2, d2, e2); ++m2; }
-                if (e3 <= ustar) { YK_CAND_SET(m2, d3, e3); ++m2; }
+                float e0 = l0, e1 = l1, e2 = l2, e3 = l3;
+                if (e0 <= ustar_f) { YK_CAND_SET(m2, d0, e0); ++m2; }
+                if (e1 <= ustar_f) { YK_CAND_SET(m2, d1, e1); ++m2; }
+                if (e2 <= ustar_f) { YK_CAND_SET(m2, d2, e2); ++m2; }
+                if (e3 <= ustar_f) { YK_CAND_SET(m2, d3, e3); ++m2; }
                 nc = m2;
               }
               if (nc < 4) {
-                YK_CAND_SET(nc, id, lb);
+                YK_CAND_SET(nc, id, __double2float_rd(lb));
                 ++nc;
               } else {
                 overflow = true;
@@ -445,11 +481,14 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         if (overflow) {
           linear = true;
         } else {
-          // exact evaluation of the survivors, all lanes in step
-          if (nc > 0 && l0 <= ustar) exact_candidate(ka.geo, c0, o, d, a, ka.t_min, hit);
-          if (nc > 1 && l1 <= ustar) exact_candidate(ka.geo, c1, o, d, a, ka.t_min, hit);
-          if (nc > 2 && l2 <= ustar) exact_candidate(ka.geo, c2, o, d, a, ka.t_min, hit);
-          if (nc > 3 && l3 <= ustar) exact_candidate(ka.geo, c3, o, d, a, ka.t_min, hit);
+          // exact evaluation of the survivors, all lanes in step; the roots' divisor a is the
+          // same for every candidate, so its refined reciprocal is computed once
+          const bool a_ok = ykd::div_range(a);
+          const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
+          if (nc > 0 && l0 <= ustar_f) exact_candidate(ka.geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 1 && l1 <= ustar_f) exact_candidate(ka.geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 2 && l2 <= ustar_f) exact_candidate(ka.geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 3 && l3 <= ustar_f) exact_candidate(ka.geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
         }
       }
       if (linear) {
@@ -483,15 +522,18 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         m = ka.mat[hid];
         // hit record (sphere.hpp:41-45, hittable.hpp:23-27)
         p = ykd::add(o, ykd::mul(d, T));
-        const v3 outward = ykd::divs(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
+        const v3 outward = ykd::divs_fast(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
         front = ykd::dot(d, outward) < 0;
         nrm = front ? outward : ykd::neg(outward);
         if (m.kind == YK_MATERIAL_LAMBERTIAN) vn = ykd::random_vec(g, -1, 1);  // vec3.hpp:134-142
       }
       const double len = ykd::nsqrt_c(ykd::len2(vn), n_ncall, n_nit);  // vec3::length(), vec3.hpp:127
+      // vn / len is what every branch below divides (sky: d.y / len; lambertian: the random
+      // vector; metal, dielectric: d), so it is computed once here, not once per branch
+      const v3 un = ykd::divs_fast(vn, len);
       if (hid < 0) {
         // sky (raytracer.hpp:35-36): t = (normalized(dir).y + 1)/2, lerp white → (.5,.7,1)
-        const double t = (d.y / len + 1.0) / 2;
+        const double t = (un.y + 1.0) / 2;
         L_r = (1.0 - t) * 1.0 + t * 0.5;
         L_g = (1.0 - t) * 1.0 + t * 0.7;
         L_b = (1.0 - t) * 1.0 + t * 1.0;
@@ -500,13 +542,13 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         bool scattered = true, push = true;
         v3 nd;
         if (m.kind == YK_MATERIAL_LAMBERTIAN) {  // material.hpp:50-59
-          nd = ykd::add(nrm, ykd::divs(vn, len));
+          nd = ykd::add(nrm, un);
           if (ykd::near_zero(nd)) nd = nrm;
         } else if (m.kind == YK_MATERIAL_METAL) {  // material.hpp:67-75 (+ fuzz extension)
-          nd = ykd::reflect(ykd::divs(d, len), nrm);
+          nd = ykd::reflect(un, nrm);
           if (m.fuzz > 0) {  // random_in_unit_sphere, material.hpp:27-30
             v3 ru = ykd::random_vec(g, -1, 1);
-            ru = ykd::divs(ru, ykd::nsqrt_c(ykd::len2(ru), n_ncall, n_nit));
+            ru = ykd::divs_fast(ru, ykd::nsqrt_c(ykd::len2(ru), n_ncall, n_nit));
             const double k = ykd::uniform(g, 0.01, 0.99);
             nd = ykd::add(nd, ykd::mul(ykd::mul(ru, k), m.fuzz));
           }
@@ -514,7 +556,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
         } else {  // dielectric extension (attenuation (1,1,1): multiplying by 1.0 is exact)
           push = false;
           const double ratio = front ? (1.0 / m.ior) : m.ior;
-          const v3 unit = ykd::divs(d, len);
+          const v3 unit = un;
           double ct = ykd::dot(ykd::neg(unit), nrm);
           if (!(ct < 1.0)) ct = 1.0;
           const double sn = ykd::nsqrt_c(1.0 - ct * ct, n_ncall, n_nit);
@@ -591,7 +633,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_persistent(KernelArgs ka) {
   if (lane == 0)
     for (int k = 0; k < 6; ++k) atomicAdd(&ka.counters[8 + k], (unsigned long long)st_acc[k]);
 #endif
-  if (ka.flags & YK_FLAG_COUNT_WORK) {
+  if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
     atomicAdd(&ka.counters[1], (unsigned long long)n_test);
     atomicAdd(&ka.counters[2], (unsigned long long)n_sqrt);
@@ -720,6 +762,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.warm = ctx->d_warm;
   ka.t_min = p->t_min;
   ka.origin_bound = ctx->origin_bound;
+  ka.inv_w = 1.0 / (double)ka.W;
+  ka.inv_h = 1.0 / (double)ka.H;
   ka.bvh_root = ctx->bvh_root;
   ka.n_nodes = ctx->n_nodes;
   ka.lds_geo_off = ctx->lds_geo_off;
@@ -757,10 +801,15 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.pix_base = p0;
     ka.npix = cnt;
     YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
-    if (ctx->scene_in_lds)
-      hipLaunchKernelGGL(yk_render_persistent<true>, dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+    const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
+    if (ctx->scene_in_lds && count)
+      hipLaunchKernelGGL((yk_render_persistent<true, true>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+    else if (ctx->scene_in_lds)
+      hipLaunchKernelGGL((yk_render_persistent<true, false>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+    else if (count)
+      hipLaunchKernelGGL((yk_render_persistent<false, true>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
     else
-      hipLaunchKernelGGL(yk_render_persistent<false>, dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+      hipLaunchKernelGGL((yk_render_persistent<false, false>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
     YK_HIP(hipGetLastError());
     ++launches;
   }
@@ -829,10 +878,9 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   auto* ctx = new ykgpu_context();
   ctx->device = device;
   ctx->cus = prop.multiProcessorCount;
-  (void)hipFuncSetAttribute((const void*)yk_render_persistent<true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)yk_render_persistent<false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (const void* k : {(const void*)yk_render_persistent<true, false>, (const void*)yk_render_persistent<false, false>,
+                        (const void*)yk_render_persistent<true, true>, (const void*)yk_render_persistent<false, true>})
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_counter, 16) != hipSuccess ||
@@ -936,8 +984,8 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   ctx->lds_bytes = ctx->lds_stack_off + ctx->stack_depth * kBlock * (uint32_t)sizeof(int32_t);
   int per_cu = 0;
   hipError_t e = ctx->scene_in_lds
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<true>, kBlock, ctx->lds_bytes)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<false>, kBlock, ctx->lds_bytes);
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<true, false>, kBlock, ctx->lds_bytes)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<false, false>, kBlock, ctx->lds_bytes);
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
   ctx->grid = per_cu * ctx->cus;
   YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));
@@ -1016,6 +1064,26 @@ int ykgpu_math_sqrt(ykgpu_context* ctx, const double* in, double* out, uint64_t 
   if (e == hipSuccess) e = hipMemcpy(out, d + n, n * sizeof(double), hipMemcpyDeviceToHost);
   (void)hipFree(d);
   if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_math_sqrt: ") + hipGetErrorString(e));
+  return YK_OK;
+}
+
+int ykgpu_math_div(ykgpu_context* ctx, const double* num3, const double* den, double* out3, uint64_t n) {
+  if (!ctx || (n && (!num3 || !den || !out3))) return fail(YK_ERR_INVALID, "null argument");
+  if (n == 0) return YK_OK;
+  YK_HIP(hipSetDevice(ctx->device));
+  double* d = nullptr;
+  YK_HIP(hipMalloc(&d, 7 * n * sizeof(double)));
+  hipError_t e = hipMemcpy(d, num3, 3 * n * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d + 3 * n, den, n * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(yk_math_div, dim3((uint32_t)blocks), dim3(256), 0, ctx->stream, d, d + 3 * n, d + 4 * n, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out3, d + 4 * n, 3 * n * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_math_div: ") + hipGetErrorString(e));
   return YK_OK;
 }
 
