@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 1u
+#define YKGPU_ABI_VERSION 2u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 and DIELECTRIC are extensions needed by BASELINE configs 2-5 (no
@@ -118,8 +118,12 @@ typedef struct yk_render_stats {
   uint64_t linear_scans;   /* segments served by the exact linear scan (flag COUNT_WORK)*/
   uint64_t newton_calls;   /* math::sqrt evaluations (flag COUNT_WORK)                 */
   uint64_t newton_iters;   /* math::sqrt loop iterations (flag COUNT_WORK)             */
-  uint64_t phase_cycles[6];/* diagnostic builds only (YK_ABLATE & 8): wave-cycles in refill,
-                              sample start, traversal, candidates, shading, path end      */
+  uint64_t phase_cycles[8];/* diagnostic builds only (YK_ABLATE & 8): wave-cycles in refill,
+                              sample start, traversal (interior nodes), candidates, shading,
+                              path end, traversal (leaves), unused                        */
+  uint64_t timeline[3];    /* diagnostic builds only: s_memrealtime (100 MHz) of the first wave start, of
+                              the first refill that found no pixel left, of the last wave
+                              exit (last launch of the call)                              */
   uint32_t launches;       /* path-tracing launches in the call                        */
   uint32_t grid_blocks;    /* persistent grid size                                     */
 } yk_render_stats;

@@ -1,0 +1,37 @@
+"""A/B wall time of library variants on the headline workload at a chosen spp (production
+instance, flags=0): one subprocess per variant run (one library per process), interleaved.
+usage: python tools/abtime.py <spp> <variant> [<variant> ...]   (variant 'base' = lib/libykgpu.so,
+otherwise lib/abl/libykgpu_<variant>.so)"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CODE = r'''
+import sys, time, json
+sys.path.insert(0, %r)
+import torch
+import uecraytracing_amd as yk
+from uecraytracing_amd.records import make_params
+arr, cam = yk.build_scene("final", 42)
+r = yk.Renderer(0); r.set_scene(arr, cam)
+p = make_params(1920, None, int(sys.argv[1]), 50, 404, flags=0)
+img = r.render(p); ts = []
+for _ in range(int(sys.argv[2])):
+    t = time.perf_counter(); r.render(p); ts.append(time.perf_counter() - t)
+import hashlib
+print(json.dumps({"ms": round(min(ts) * 1e3, 3), "kernel_ms": round(r.stats()["kernel_ms"], 3),
+                  "sha": hashlib.sha256(img.tobytes()).hexdigest()[:12]}))
+''' % ROOT
+spp = sys.argv[1]
+reps = os.environ.get("AB_REPS", "3")
+names = sys.argv[2:] or ["base"]
+for rnd in range(2):
+    for name in names:
+        lib = os.path.join(ROOT, "uecraytracing_amd/lib/libykgpu.so") if name == "base" else \
+            os.path.join(ROOT, f"uecraytracing_amd/lib/abl/libykgpu_{name}.so")
+        env = dict(os.environ, YKGPU_LIB_OVERRIDE=lib)
+        out = subprocess.run([sys.executable, "-c", CODE, spp, reps], env=env, capture_output=True, text=True)
+        line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+        print(rnd, name, line[-1] if line else out.stderr[-400:], flush=True)

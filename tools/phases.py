@@ -11,6 +11,18 @@ with yk.Renderer(0) as r:
     p = make_params(1920, None, spp, 50, 404, flags=1)
     r.render(p); r.render(p)
     st = r.stats()
-    pc = st["phase_cycles"]; tot = sum(pc) or 1
-    names = ["refill", "start", "traversal", "candidates", "shade", "path_end"]
+    pc = st["phase_cycles"]
+    node_iters = pc[7]
+    pc = pc[:7]; tot = sum(pc) or 1
+    names = ["refill", "start", "trav_nodes", "candidates", "shade", "path_end", "trav_leaves", "-"]
     print(scene, f"kernels {st['kernel_ms']:.1f} ms", " ".join(f"{n}={c/tot*100:.1f}%" for n, c in zip(names, pc)))
+    tl = st["timeline"]
+    if tl[0] and tl[2] > tl[0]:
+        span = tl[2] - tl[0]
+        print(f"timeline: pixels exhausted at {(tl[1] - tl[0]) / span * 100:.1f}% of the launch "
+              f"({span / 1e5:.1f} ms), tail {(tl[2] - tl[1]) / span * 100:.1f}%")
+    r.render(make_params(1920, None, spp, 50, 404, flags=1))
+    st2 = r.stats()
+    print(f"node visits (lanes) {st2['node_visits']}, wave-level node-loop iterations {node_iters} -> "
+          f"lane utilisation in the node loop {st2['node_visits'] / max(1, node_iters * 64):.3f}; "
+          f"wave-cycles per node iteration {pc[2] / max(1, node_iters):.0f}")

@@ -10,7 +10,7 @@ scene = sys.argv[1] if len(sys.argv) > 1 else "final"
 arr, cam = yk.build_scene(scene, 42)
 with yk.Renderer(0) as r:
     r.set_scene(arr, cam)
-    for (W, spp) in ((192, 16), (480, 32), (1920, 16)):
+    for (W, spp) in [tuple(map(int, a.split("x"))) for a in (sys.argv[2:] or ["192x16", "480x32", "1920x16"])]:
         p = make_params(W, None, spp, 50, 404, flags=1)
         r.render(p)
         t = time.time()

@@ -32,6 +32,8 @@ static_assert(sizeof(Node) == 64, "Node layout");
 // read per axis returns the planes already ordered, so the slab test needs no min/max
 // (rounding is monotonic, so the selection equals min/max of the two products).  child >= 0 is
 // the BYTE OFFSET of an inner node (no multiply per visit); leaves keep their negative codes.
+// (80 bytes matters: with the 485-sphere scene, nodes + geometry + stacks of a 256-thread block
+// fit 3 blocks per CU in 160 KB of LDS; an 88-byte node with a second child copy does not.)
 struct alignas(16) SlabNode {
   float x[6], y[6], z[6];
   int32_t child[2];

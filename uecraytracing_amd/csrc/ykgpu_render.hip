@@ -76,7 +76,7 @@ static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 #define YK_WAVES_PER_EU 0
 #endif
 constexpr int kBlock = YK_BLOCK;
-constexpr int kCounters = 16;
+constexpr int kCounters = 20;  // [16..18]: timeline (diagnostic builds)
 
 // Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
 // points, summed per phase into counters[8..13] (refill, start, traversal, candidates, shade,
@@ -104,7 +104,9 @@ struct KernelArgs {
   uint32_t W, H, spp, max_depth;
   uint32_t seed0, row_begin, row_count, row_stride;
   uint32_t nspheres, npix, flags, id_stride;
-  uint32_t pix_base, pad1;          // this launch renders tile pixels [pix_base, pix_base + npix)
+  uint32_t pix_base;                // this launch takes processing slots [pix_base, pix_base + npix)
+  uint32_t pix_total;               // processing slots of the call
+  const uint32_t* __restrict__ order;  // slot → tile pixel (kNoPixel: empty slot of an edge tile)
   const uint32_t* __restrict__ warm;  // x_397 per sample of the launch, [(pix - pix_base)*spp + s]
   double t_min;
   double inv_w, inv_h;  // RN(1/W), RN(1/H) for the camera's exact divisions (div_markstein)
@@ -211,10 +213,16 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
 
 __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
 
+// Processing order: slot p of a call renders tile pixel order[p] (ykgpu_context::order, built on
+// the host for the image geometry): 8x8 pixel blocks, so the lanes a wave refills together take
+// neighbouring pixels in both directions.  Every pixel's samples are independent of the order.
+constexpr uint32_t kNoPixel = 0xffffffffu;
+
 // Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread,
 // one 16-B store.  out[i] = x_397(seed(i)), i = (pix - pix_base) * spp + s.
 struct WarmArgs {
-  uint32_t W, spp, seed0, row_begin, row_stride, pix_base;
+  uint32_t W, spp, seed0, row_begin, row_stride, pix_base, pix_total, pad;
+  const uint32_t* order;
   uint64_t n;  // samples in the launch
   uint32_t* out;
 };
@@ -226,7 +234,9 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint64_t i = i0 + k < wa.n ? i0 + k : wa.n - 1;
-      const uint32_t pix = wa.pix_base + (uint32_t)(i / wa.spp), sm = (uint32_t)(i % wa.spp);
+      const uint32_t q = wa.order[wa.pix_base + (uint32_t)(i / wa.spp)];
+      const uint32_t pix = q == kNoPixel ? 0u : q;
+      const uint32_t sm = (uint32_t)(i % wa.spp);
       const uint32_t tr = pix / wa.W, xx = pix - tr * wa.W;
       const uint32_t y = wa.row_begin + tr * wa.row_stride;
       x[k] = wa.seed0 + (y * wa.W + xx) * wa.spp + sm;
@@ -278,7 +288,7 @@ void yk_render_persistent(KernelArgs ka) {
   if (kSceneInLds) {
     const uint4* src[3] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids};
     const uint32_t off[3] = {0u, ka.lds_geo_off, ka.lds_ids_off};
-    const uint32_t n16[3] = {ka.n_nodes * (uint32_t)(sizeof(ykbvh::SlabNode) / 16), ka.nspheres * 2u,
+    const uint32_t n16[3] = {(ka.n_nodes * (uint32_t)sizeof(ykbvh::SlabNode) + 15u) / 16u, ka.nspheres * 2u,
                              (ka.nspheres + 3u) / 4u};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -300,10 +310,11 @@ void yk_render_persistent(KernelArgs ka) {
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0, n_ncall = 0, n_nit = 0;
 
 #if YK_ABLATE & 8
-  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t st_prev = __builtin_amdgcn_s_memtime();
+  if (lane == 0) atomicMin(&ka.counters[16], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
-  uint32_t pix = 0, s = 0, depth = 0, nstk = 0;
+  uint32_t pix = 0, qpix = 0, s = 0, depth = 0, nstk = 0;
   uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // newest attenuation id in st0's low half
   double acc_r = 0, acc_g = 0, acc_b = 0;
   v3 o = {0, 0, 0}, d = {0, 0, 0};
@@ -318,8 +329,15 @@ void yk_render_persistent(KernelArgs ka) {
       if ((int)lane == leader) base = atomicAdd(ka.pixel_counter, (uint32_t)__popcll(m));
       base = __shfl(base, leader);
       const uint32_t mine = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-      if (mine >= ka.npix) break;
-      pix = ka.pix_base + mine;
+      if (mine >= ka.npix) {
+#if YK_ABLATE & 8
+        if ((int)lane == leader) atomicMin(&ka.counters[17], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+        break;
+      }
+      pix = ka.pix_base + mine;  // processing slot
+      qpix = ka.order[pix];      // tile pixel
+      if (qpix == kNoPixel) continue;  // empty slot of an edge block: refill again
       s = 0;
       acc_r = acc_g = acc_b = 0.0;
       have_pixel = true;
@@ -329,7 +347,7 @@ void yk_render_persistent(KernelArgs ka) {
 
     // ---- start sample s of the pixel: seed, jitter, camera ray (source.cpp:154-165) ------
     if (!in_path) {
-      const uint32_t tr = pix / ka.W, x = pix - tr * ka.W;
+      const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
       const uint32_t y = ka.row_begin + tr * ka.row_stride;
       // seed (uint32 wrap, source.cpp:154-158); x_397 comes from yk_mt_warmup
       ykd::mt_start_from(g, ka.seed0 + (y * ka.W + x) * ka.spp + s,
@@ -381,15 +399,32 @@ void yk_render_persistent(KernelArgs ka) {
         // arithmetic only, so explicit FMAs are fine here.
         const float ix = safe_rcp((float)d.x), iy = safe_rcp((float)d.y), iz = safe_rcp((float)d.z);
         const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
-        // byte offsets of this ray's (near, far) plane pairs inside a SlabNode (yk_bvh.hpp)
-        const uint32_t offx = ix < 0.0f ? 8u : 0u, offy = (iy < 0.0f ? 8u : 0u) + 24u,
-                       offz = (iz < 0.0f ? 8u : 0u) + 48u;
+        // this ray's (near, far) plane pairs inside a SlabNode (yk_bvh.hpp), as base pointers:
+        // a visit then costs one address add per axis
+        const char* const px = nodes + (ix < 0.0f ? 8u : 0u);
+        const char* const py = nodes + 24u + (iy < 0.0f ? 8u : 0u);
+        const char* const pz = nodes + 48u + (iz < 0.0f ? 8u : 0u);
+        // Conservative interval test without per-visit relaxation: far distances
+        // come out of the FMA already scaled by c = 1 + 2^-17 (scaled 1/d and o/d), near
+        // distances are compared unscaled against tmin_lo = t_min (1 - 2^-17) and against
+        // ustar_f (U* (1 + 2^-18)).  A box passes iff
+        //   max(tn, tmin_lo) <= min(tf * c, ustar_f),
+        // which holds whenever the former test with both distances relaxed by 2^-20 held.
+        constexpr float kFar = 1.0f + 0x1p-17f;
         const f2 ixv = {ix, ix}, iyv = {iy, iy}, izv = {iz, iz};
         const f2 noix = {-oix, -oix}, noiy = {-oiy, -oiy}, noiz = {-oiz, -oiz};
+        // scaled far terms: ONE rounding of the origin product, as for the near terms, so the
+        // origin perturbation stays within delta/4 (yk_bvh.hpp); the rounding of ix*c is a
+        // relative error inside the 2^-17 margin
+        const float ixs = ix * kFar, iys = iy * kFar, izs = iz * kFar;
+        const f2 ixc = {ixs, ixs}, iyc = {iys, iys}, izc = {izs, izs};
+        const float ox_f = (float)o.x, oy_f = (float)o.y, oz_f = (float)o.z;
+        const f2 noixc = {-(ox_f * ixs), -(ox_f * ixs)}, noiyc = {-(oy_f * iys), -(oy_f * iys)},
+                 noizc = {-(oz_f * izs), -(oz_f * izs)};
         const double ia = ykd::rcp_bound(a);  // bounds only: relative error < 2^-44
-        const float tminf = (float)ka.t_min;
+        const float tmin_lo = __double2float_rd(ka.t_min) * (1.0f - 0x1p-17f);
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
-        float ustar_f = INFINITY;
+        float ustar_f = INFINITY;  // >= ustar * (1 + 2^-18)
         uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
         // candidate lower bounds kept as floats rounded down, compared with ustar_f (>= U*):
         // both only ever keep MORE candidates than the double comparison would
@@ -399,27 +434,31 @@ void yk_render_persistent(KernelArgs ka) {
         uint32_t sp = 0;
         for (;;) {
           if (node >= 0) {
-            ++n_node;
-            const char* nb = nodes + node;
-            // (near, far) planes of both children per axis, one packed FMA per pair:
+            if (kCount) ++n_node;
+#if YK_ABLATE & 8
+            // wave-level iterations of the interior-node loop (diagnostic): the first active
+            // lane counts
+            if ((uint32_t)__builtin_ctzll(__ballot(1)) == lane) ++st_acc[7];
+#endif
+            // near / far distances of both children per axis, one packed FMA per pair:
             // t = plane*(1/d) - o*(1/d)
-            const f2 nx = __builtin_elementwise_fma(*(const f2*)(nb + offx), ixv, noix);
-            const f2 fx = __builtin_elementwise_fma(*(const f2*)(nb + offx + 8), ixv, noix);
-            const f2 ny = __builtin_elementwise_fma(*(const f2*)(nb + offy), iyv, noiy);
-            const f2 fy = __builtin_elementwise_fma(*(const f2*)(nb + offy + 8), iyv, noiy);
-            const f2 nz = __builtin_elementwise_fma(*(const f2*)(nb + offz), izv, noiz);
-            const f2 fz = __builtin_elementwise_fma(*(const f2*)(nb + offz + 8), izv, noiz);
-            const int2 ch = *(const int2*)(nb + 72);
-            float tn[2], tf[2];
+            const char* const ax = px + node;
+            const f2 nx = __builtin_elementwise_fma(*(const f2*)(ax), ixv, noix);
+            const f2 fx = __builtin_elementwise_fma(*(const f2*)(ax + 8), ixc, noixc);
+            const f2 ny = __builtin_elementwise_fma(*(const f2*)(py + node), iyv, noiy);
+            const f2 fy = __builtin_elementwise_fma(*(const f2*)(py + node + 8), iyc, noiyc);
+            const f2 nz = __builtin_elementwise_fma(*(const f2*)(pz + node), izv, noiz);
+            const f2 fz = __builtin_elementwise_fma(*(const f2*)(pz + node + 8), izc, noizc);
+            const int2 ch = *(const int2*)(nodes + node + 72);
+            float tn[2];
+            bool hk[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-              const float n0 = fmaxf(fmaxf(nx[k], ny[k]), nz[k]);
-              const float f0 = fminf(fminf(fx[k], fy[k]), fz[k]);
-              tn[k] = __builtin_fmaf(-fabsf(n0), 0x1p-20f, n0);  // relax by the error bound
-              tf[k] = __builtin_fmaf(fabsf(f0), 0x1p-20f, f0);
+              tn[k] = fmaxf(fmaxf(fmaxf(nx[k], ny[k]), nz[k]), tmin_lo);
+              const float tf = fminf(fminf(fminf(fx[k], fy[k]), fz[k]), ustar_f);
+              hk[k] = tn[k] <= tf;
             }
-            const bool h0 = tn[0] <= tf[0] && tf[0] >= tminf && tn[0] <= ustar_f;
-            const bool h1 = tn[1] <= tf[1] && tf[1] >= tminf && tn[1] <= ustar_f;
+            const bool h0 = hk[0], h1 = hk[1];
             if (h0 && h1) {
               const bool first0 = tn[0] <= tn[1];
               stk[sp * kBlock] = first0 ? ch.y : ch.x;
@@ -432,6 +471,7 @@ void yk_render_persistent(KernelArgs ka) {
               continue;
             }
           } else {
+            YK_STAMP(2);  // interior nodes since the last stamp
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
             for (uint32_t k = 0; k < cnt; ++k) {
               const SphereGeo sg = leaf_geo[first + k];
@@ -452,7 +492,7 @@ void yk_render_persistent(KernelArgs ka) {
               if (!(lb <= ustar)) continue;
               if (ub < ustar) {
                 ustar = ub;
-                ustar_f = (float)ub * (1.0f + 0x1p-20f);
+                ustar_f = (float)ub * (1.0f + 0x1p-18f);
               }
               const uint32_t id = leaf_ids[first + k];
               if (nc == 4) {  // compact: drop entries the new bound has excluded
@@ -472,6 +512,7 @@ void yk_render_persistent(KernelArgs ka) {
                 overflow = true;
               }
             }
+            YK_STAMP(6);  // this leaf
           }
           if (sp == 0) break;
           --sp;
@@ -609,7 +650,7 @@ void yk_render_persistent(KernelArgs ka) {
       in_path = false;
       if (++s == ka.spp) {
         // to_color3b (source.cpp:73-83): /spp, math::sqrt, clamp [0, .999], *256, truncate
-        const size_t o3 = (size_t)pix * 3;
+        const size_t o3 = (size_t)qpix * 3;
         const double spp = (double)ka.spp;
         double q[3] = {acc_r, acc_g, acc_b};
         if (ka.sums) {
@@ -631,7 +672,9 @@ void yk_render_persistent(KernelArgs ka) {
 
 #if YK_ABLATE & 8
   if (lane == 0)
-    for (int k = 0; k < 6; ++k) atomicAdd(&ka.counters[8 + k], (unsigned long long)st_acc[k]);
+    for (int k = 0; k < 7; ++k) atomicAdd(&ka.counters[8 + k], (unsigned long long)st_acc[k]);
+  atomicAdd(&ka.counters[15], (unsigned long long)st_acc[7]);  // per-lane partial counts
+  if (lane == 0) atomicMax(&ka.counters[18], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
   if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
@@ -659,6 +702,8 @@ struct ykgpu_context {
   uint32_t lds_bytes = 0, lds_geo_off = 0, lds_ids_off = 0, lds_stack_off = 0, stack_depth = 0;
   uint32_t n_nodes = 0;
   uint32_t* d_warm = nullptr;  // x_397 per sample of one chunk
+  uint32_t* d_order = nullptr;  // processing slot → tile pixel, for (order_w, order_rows)
+  uint32_t order_w = 0, order_rows = 0, order_slots = 0;
   size_t warm_cap = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -728,13 +773,48 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
 }
 
 constexpr uint64_t kWarmChunkSamples = 1ull << 30;  // 4 GiB of x_397 per launch at most
+#ifndef YK_TILE
+#define YK_TILE 8
+#endif
+constexpr uint32_t kTile = YK_TILE;  // processing blocks of kTile x kTile pixels (0: row-major)
+
+// The processing order of a tile of W x rows pixels (kernel comment at kNoPixel).  A function of
+// the geometry only, so it is built once per size and kept on the device.
+int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows) {
+  if (ctx->d_order && ctx->order_w == W && ctx->order_rows == rows) return YK_OK;
+  std::vector<uint32_t> ord;
+  if (kTile == 0) {
+    ord.resize((size_t)W * rows);
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (uint32_t)i;
+  } else {
+    const uint32_t bx = (W + kTile - 1) / kTile, by = (rows + kTile - 1) / kTile;
+    ord.reserve((size_t)bx * by * kTile * kTile);
+    for (uint32_t j = 0; j < by; ++j)
+      for (uint32_t i = 0; i < bx; ++i)
+        for (uint32_t k = 0; k < kTile * kTile; ++k) {
+          const uint32_t x = i * kTile + k % kTile, y = j * kTile + k / kTile;
+          ord.push_back(x < W && y < rows ? y * W + x : kNoPixel);
+        }
+  }
+  (void)hipFree(ctx->d_order);
+  ctx->d_order = nullptr;
+  ctx->order_w = ctx->order_rows = ctx->order_slots = 0;
+  YK_HIP(hipMalloc(&ctx->d_order, ord.size() * sizeof(uint32_t)));
+  YK_HIP(hipMemcpy(ctx->d_order, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  ctx->order_w = W;
+  ctx->order_rows = rows;
+  ctx->order_slots = (uint32_t)ord.size();
+  return YK_OK;
+}
 
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
   int rc = ensure_scratch(ctx, p->max_depth);
   if (rc) return rc;
-  const uint32_t npix_total = p->row_count * p->image_width;
-  const uint64_t total = (uint64_t)npix_total * p->samples_per_pixel;
+  rc = ensure_order(ctx, p->image_width, p->row_count);
+  if (rc) return rc;
+  const uint32_t npix_total = ctx->order_slots;  // processing slots (>= pixels)
+  const uint64_t total = (uint64_t)npix_total * p->samples_per_pixel;  // sample slots
   const uint32_t chunk_pix =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npix_total, kWarmChunkSamples / p->samples_per_pixel));
   const size_t warm_need = (size_t)std::min<uint64_t>(total, (uint64_t)chunk_pix * p->samples_per_pixel);
@@ -758,8 +838,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.nspheres = ctx->nspheres;
   ka.flags = p->flags;
   ka.id_stride = ctx->id_stride;
-  ka.pad1 = 0;
   ka.warm = ctx->d_warm;
+  ka.order = ctx->d_order;
   ka.t_min = p->t_min;
   ka.origin_bound = ctx->origin_bound;
   ka.inv_w = 1.0 / (double)ka.W;
@@ -788,7 +868,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.row_begin = p->row_begin;
   wa.row_stride = p->row_stride;
   wa.out = ctx->d_warm;
+  wa.pix_total = npix_total;
+  wa.pad = 0;
+  wa.order = ctx->d_order;
+  ka.pix_total = npix_total;
   YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
+  YK_HIP(hipMemsetAsync(ctx->d_stats + 16, 0xff, 2 * sizeof(unsigned long long), st));  // minima
   YK_HIP(hipEventRecord(ctx->ev0, st));
   uint32_t launches = 0;
   for (uint32_t p0 = 0; p0 < npix_total; p0 += chunk_pix) {
@@ -815,7 +900,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   }
   YK_HIP(hipEventRecord(ctx->ev1, st));
   ctx->stats = yk_render_stats{};
-  ctx->stats.samples = total;
+  ctx->stats.samples = (uint64_t)p->row_count * p->image_width * p->samples_per_pixel;
   ctx->stats.launches = launches;
   ctx->stats.grid_blocks = (uint32_t)ctx->grid;
   ctx->stats_pending = true;
@@ -833,7 +918,8 @@ int finish_stats(ykgpu_context* ctx) {
   ctx->stats.linear_scans = c[5];
   ctx->stats.newton_calls = c[6];
   ctx->stats.newton_iters = c[7];
-  for (int k = 0; k < 6; ++k) ctx->stats.phase_cycles[k] = c[8 + k];
+  for (int k = 0; k < 8; ++k) ctx->stats.phase_cycles[k] = c[8 + k];
+  for (int k = 0; k < 3; ++k) ctx->stats.timeline[k] = c[16 + k];
   ctx->stats.kernel_ms = ms;
   ctx->stats.segments = c[0];
   ctx->stats.sphere_tests = c[1];
@@ -901,6 +987,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_counter);
   (void)hipFree(ctx->d_stats);
   (void)hipFree(ctx->d_warm);
+  (void)hipFree(ctx->d_order);
   (void)hipFree(ctx->d_nodes);
   (void)hipFree(ctx->d_leaf_geo);
   (void)hipFree(ctx->d_leaf_ids);

@@ -95,7 +95,8 @@ class RenderStats(ctypes.Structure):
         ("linear_scans", ctypes.c_uint64),
         ("newton_calls", ctypes.c_uint64),
         ("newton_iters", ctypes.c_uint64),
-        ("phase_cycles", ctypes.c_uint64 * 6),
+        ("phase_cycles", ctypes.c_uint64 * 8),
+        ("timeline", ctypes.c_uint64 * 3),
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
     ]
@@ -103,6 +104,7 @@ class RenderStats(ctypes.Structure):
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
         d["phase_cycles"] = list(self.phase_cycles)
+        d["timeline"] = list(self.timeline)
         return d
 
 
