@@ -97,17 +97,19 @@ constexpr int kCounters = 20;  // [16..18]: timeline (diagnostic builds)
   } while (0)
 #endif
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
+constexpr uint32_t kClaim = 128;    // sample slots a wave claims per atomic
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 
 struct KernelArgs {
   yk_camera cam;
   uint32_t W, H, spp, max_depth;
   uint32_t seed0, row_begin, row_count, row_stride;
-  uint32_t nspheres, npix, flags, id_stride;
-  uint32_t pix_base;                // this launch takes processing slots [pix_base, pix_base + npix)
-  uint32_t pix_total;               // processing slots of the call
-  const uint32_t* __restrict__ order;  // slot → tile pixel (kNoPixel: empty slot of an edge tile)
-  const uint32_t* __restrict__ warm;  // x_397 per sample of the launch, [(pix - pix_base)*spp + s]
+  uint32_t nspheres, pad_n, flags, id_stride;
+  // A launch renders samples [s0, s0 + nsl / npix_slots) of every pixel: sample slot
+  // i = s_local * npix_slots + p is sample s0 + s_local of tile pixel order[p].
+  uint32_t s0, nsl, npix_slots, pad_s;
+  const uint32_t* __restrict__ order;  // p → tile pixel (kNoPixel: empty slot of an edge block)
+  const uint32_t* __restrict__ warm;   // x_397 per sample slot of the launch
   double t_min;
   double inv_w, inv_h;  // RN(1/W), RN(1/H) for the camera's exact divisions (div_markstein)
   double origin_bound;  // |o|_inf beyond which the BVH's float culling is not proven sound
@@ -119,9 +121,8 @@ struct KernelArgs {
   const uint32_t* __restrict__ leaf_ids;   // leaf slot → tuple index
   const SphereGeo* __restrict__ geo;
   const SphereMat* __restrict__ mat;
-  uint8_t* rgb;
-  double* sums;
-  uint32_t* pixel_counter;
+  double* col;                       // sample colours, SoA: col[c * nsl + i]
+  uint32_t* pixel_counter;           // sample-slot counter
   uint32_t* mt_scratch;
   uint16_t* id_scratch;
   unsigned long long* counters;  // [segments, sphere_tests, sqrt_calls, mt_fallbacks, nodes]
@@ -221,9 +222,9 @@ constexpr uint32_t kNoPixel = 0xffffffffu;
 // Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread,
 // one 16-B store.  out[i] = x_397(seed(i)), i = (pix - pix_base) * spp + s.
 struct WarmArgs {
-  uint32_t W, spp, seed0, row_begin, row_stride, pix_base, pix_total, pad;
+  uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, pad;
   const uint32_t* order;
-  uint64_t n;  // samples in the launch
+  uint64_t n;  // sample slots in the launch
   uint32_t* out;
 };
 
@@ -234,9 +235,10 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint64_t i = i0 + k < wa.n ? i0 + k : wa.n - 1;
-      const uint32_t q = wa.order[wa.pix_base + (uint32_t)(i / wa.spp)];
+      const uint32_t sl = (uint32_t)(i / wa.npix_slots), pp = (uint32_t)(i - (uint64_t)sl * wa.npix_slots);
+      const uint32_t q = wa.order[pp];
       const uint32_t pix = q == kNoPixel ? 0u : q;
-      const uint32_t sm = (uint32_t)(i % wa.spp);
+      const uint32_t sm = wa.s0 + sl;
       const uint32_t tr = pix / wa.W, xx = pix - tr * wa.W;
       const uint32_t y = wa.row_begin + tr * wa.row_stride;
       x[k] = wa.seed0 + (y * wa.W + xx) * wa.spp + sm;
@@ -253,6 +255,48 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 // kSceneInLds: the BVH nodes, the leaf-ordered sphere geometry and the leaf→tuple ids are copied
 // into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
+
+// Ordered sum of a launch's sample colours per pixel: pixel_color of source.cpp:137-167 is the
+// left fold ((0 + c_0) + c_1) + ... in sample order, continued across launches through acc; after
+// the last launch, to_color3b (source.cpp:73-83): /spp, math::sqrt, clamp [0, .999], *256,
+// truncate.  One thread per processing slot, coalesced over the SoA colours.
+struct ReduceArgs {
+  const double* col;  // col[c * nsl + s_local * npix_slots + p]
+  double* acc;        // running sums, acc[c * npix_slots + p]
+  const uint32_t* order;
+  uint8_t* rgb;
+  double* sums;
+  uint32_t npix_slots, nsl, ks, spp;
+  uint32_t first, last, pad0, pad1;
+};
+__global__ __launch_bounds__(256) void yk_reduce_samples(ReduceArgs ra) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ra.npix_slots) return;
+  const uint32_t q = ra.order[p];
+  if (q == kNoPixel) return;
+  double a[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) a[c] = ra.first ? 0.0 : ra.acc[(size_t)c * ra.npix_slots + p];
+  for (uint32_t k = 0; k < ra.ks; ++k) {
+    const size_t i = (size_t)k * ra.npix_slots + p;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[(size_t)c * ra.nsl + i];
+  }
+  if (!ra.last) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) ra.acc[(size_t)c * ra.npix_slots + p] = a[c];
+    return;
+  }
+  const size_t o3 = (size_t)q * 3;
+  const double spp = (double)ra.spp;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (ra.sums) ra.sums[o3 + c] = a[c];
+    double v = ykd::nsqrt(a[c] / spp);
+    v = (v < 0.0) ? 0.0 : (0.999 < v) ? 0.999 : v;
+    ra.rgb[o3 + c] = (uint8_t)(uint32_t)(v * 256);
+  }
+}
 
 // ykgpu_math_div: the renderer's vector / scalar division (divs_fast) on a buffer (diagnostic).
 __global__ __launch_bounds__(256) void yk_math_div(const double* num3, const double* den, double* out3,
@@ -314,44 +358,65 @@ void yk_render_persistent(KernelArgs ka) {
   uint64_t st_prev = __builtin_amdgcn_s_memtime();
   if (lane == 0) atomicMin(&ka.counters[16], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
-  uint32_t pix = 0, qpix = 0, s = 0, depth = 0, nstk = 0;
+  uint32_t slot = 0, depth = 0, nstk = 0;
   uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // newest attenuation id in st0's low half
-  double acc_r = 0, acc_g = 0, acc_b = 0;
   v3 o = {0, 0, 0}, d = {0, 0, 0};
-  bool have_pixel = false, in_path = false;
+  bool in_path = false;
+  // wave-level reserve of claimed sample slots (identical in every lane of the wave)
+  uint32_t res_base = 0, res_left = 0;
 
   for (;;) {
-    // ---- refill: lanes without a pixel take the next ones, one atomic per wave ----------
-    if (!have_pixel) {
-      const unsigned long long m = __ballot(1);
-      const int leader = __ffsll((long long)m) - 1;
-      uint32_t base = 0;
-      if ((int)lane == leader) base = atomicAdd(ka.pixel_counter, (uint32_t)__popcll(m));
-      base = __shfl(base, leader);
-      const uint32_t mine = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-      if (mine >= ka.npix) {
-#if YK_ABLATE & 8
-        if ((int)lane == leader) atomicMin(&ka.counters[17], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
-        break;
+    // ---- refill: lanes without a path take the next sample slots from the wave's reserve;
+    //      one atomic per kClaim slots.  Every lane runs this block, so the reserve stays
+    //      uniform.  (A pixel is no longer a lane's unit of work: the samples of a pixel are
+    //      independent, only their SUM is ordered, and that is done by yk_reduce_samples.)
+    {
+      const unsigned long long m = __ballot(!in_path);
+      if (m) {
+        const uint32_t need = (uint32_t)__popcll(m);
+        uint32_t fresh = 0;
+        if (res_left < need) {
+          const int leader = __ffsll((long long)m) - 1;
+          if ((int)lane == leader) fresh = atomicAdd(ka.pixel_counter, kClaim);
+          fresh = __shfl(fresh, leader);
+        }
+        if (!in_path) {
+          const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+          slot = r < res_left ? res_base + r : fresh + (r - res_left);
+        }
+        if (res_left < need) {
+          res_base = fresh + (need - res_left);
+          res_left = kClaim - (need - res_left);
+        } else {
+          res_base += need;
+          res_left -= need;
+        }
       }
-      pix = ka.pix_base + mine;  // processing slot
-      qpix = ka.order[pix];      // tile pixel
-      if (qpix == kNoPixel) continue;  // empty slot of an edge block: refill again
-      s = 0;
-      acc_r = acc_g = acc_b = 0.0;
-      have_pixel = true;
-      in_path = false;
+      if (!in_path) {
+        if (slot >= ka.nsl) {
+#if YK_ABLATE & 8
+          atomicMin(&ka.counters[17], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+          break;
+        }
+      }
     }
     YK_STAMP(0);
 
     // ---- start sample s of the pixel: seed, jitter, camera ray (source.cpp:154-165) ------
-    if (!in_path) {
+    bool start = !in_path;
+    uint32_t qpix = 0;
+    if (start) {
+      const uint32_t sl = slot / ka.npix_slots;
+      qpix = ka.order[slot - sl * ka.npix_slots];
+      start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
+    }
+    if (start) {
+      const uint32_t s = ka.s0 + slot / ka.npix_slots;
       const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
       const uint32_t y = ka.row_begin + tr * ka.row_stride;
       // seed (uint32 wrap, source.cpp:154-158); x_397 comes from yk_mt_warmup
-      ykd::mt_start_from(g, ka.seed0 + (y * ka.W + x) * ka.spp + s,
-                         ka.warm[(size_t)(pix - ka.pix_base) * ka.spp + s]);
+      ykd::mt_start_from(g, ka.seed0 + (y * ka.W + x) * ka.spp + s, ka.warm[slot]);
       // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
       const double u = ykd::div_markstein((double)x + ykd::uniform(g, 0, 1), (double)ka.W, ka.inv_w);
       const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1), (double)ka.H, ka.inv_h);
@@ -383,7 +448,8 @@ void yk_render_persistent(KernelArgs ka) {
     // (a) closest hit: hittable_list::hit_impl (hittable_list.hpp:32-58) over
     //     sphere::hit_impl (sphere.hpp:25-48): tuple order, t_max shrinking to the last
     //     accepted root, so the closest hit wins and an exact tie goes to the later sphere.
-    const bool alive = depth != 0;  // depth == 0 → black (raytracer.hpp:23)
+    // depth == 0 → black (raytracer.hpp:23); lanes without a path (empty slot) sit this out
+    const bool alive = in_path && depth != 0;
     Hit hit{INFINITY, -1, 0, 0, 0, 0};
     if (alive) {
       ++n_seg;
@@ -548,7 +614,7 @@ void yk_render_persistent(KernelArgs ka) {
     //     (material.hpp:33-36), metal's / dielectric's normalized(dir) — so the Newton square
     //     root of that length runs once, with all those lanes together, instead of once per
     //     branch.  Each lane's own operation order is unchanged.
-    bool ended = !alive;
+    bool ended = in_path && !alive;
     double L_r = 0, L_g = 0, L_b = 0;
     if (alive) {
       const int hid = hit.hid;
@@ -644,28 +710,11 @@ void yk_render_persistent(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
-      acc_r = acc_r + L_r;  // transform_reduce, strictly in sample order
-      acc_g = acc_g + L_g;
-      acc_b = acc_b + L_b;
+      // the sample's colour; yk_reduce_samples adds them in sample order
+      ka.col[slot] = L_r;
+      ka.col[(size_t)ka.nsl + slot] = L_g;
+      ka.col[2 * (size_t)ka.nsl + slot] = L_b;
       in_path = false;
-      if (++s == ka.spp) {
-        // to_color3b (source.cpp:73-83): /spp, math::sqrt, clamp [0, .999], *256, truncate
-        const size_t o3 = (size_t)qpix * 3;
-        const double spp = (double)ka.spp;
-        double q[3] = {acc_r, acc_g, acc_b};
-        if (ka.sums) {
-          ka.sums[o3 + 0] = acc_r;
-          ka.sums[o3 + 1] = acc_g;
-          ka.sums[o3 + 2] = acc_b;
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          double vq = ykd::nsqrt_c(q[c] / spp, n_ncall, n_nit);
-          vq = (vq < 0.0) ? 0.0 : (0.999 < vq) ? 0.999 : vq;
-          ka.rgb[o3 + c] = (uint8_t)(uint32_t)(vq * 256);
-        }
-        have_pixel = false;
-      }
     }
     YK_STAMP(5);
   }
@@ -701,7 +750,10 @@ struct ykgpu_context {
   bool scene_in_lds = false;
   uint32_t lds_bytes = 0, lds_geo_off = 0, lds_ids_off = 0, lds_stack_off = 0, stack_depth = 0;
   uint32_t n_nodes = 0;
-  uint32_t* d_warm = nullptr;  // x_397 per sample of one chunk
+  uint32_t* d_warm = nullptr;  // x_397 per sample slot of one launch
+  double* d_col = nullptr;     // sample colours of one launch (SoA)
+  double* d_acc = nullptr;     // running per-pixel sums between launches
+  size_t col_cap = 0, acc_cap = 0;
   uint32_t* d_order = nullptr;  // processing slot → tile pixel, for (order_w, order_rows)
   uint32_t order_w = 0, order_rows = 0, order_slots = 0;
   size_t warm_cap = 0;
@@ -772,7 +824,7 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
   return YK_OK;
 }
 
-constexpr uint64_t kWarmChunkSamples = 1ull << 30;  // 4 GiB of x_397 per launch at most
+constexpr uint64_t kColourBytes = 3ull << 29;  // 1.5 GiB of sample colours per launch at most
 #ifndef YK_TILE
 #define YK_TILE 8
 #endif
@@ -813,18 +865,23 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   if (rc) return rc;
   rc = ensure_order(ctx, p->image_width, p->row_count);
   if (rc) return rc;
-  const uint32_t npix_total = ctx->order_slots;  // processing slots (>= pixels)
-  const uint64_t total = (uint64_t)npix_total * p->samples_per_pixel;  // sample slots
-  const uint32_t chunk_pix =
-      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(npix_total, kWarmChunkSamples / p->samples_per_pixel));
-  const size_t warm_need = (size_t)std::min<uint64_t>(total, (uint64_t)chunk_pix * p->samples_per_pixel);
-  if (warm_need > ctx->warm_cap) {
-    (void)hipFree(ctx->d_warm);
-    ctx->d_warm = nullptr;
-    ctx->warm_cap = 0;
-    YK_HIP(hipMalloc(&ctx->d_warm, warm_need * sizeof(uint32_t)));
-    ctx->warm_cap = warm_need;
-  }
+  // Launches of K samples per pixel: the colours of a launch (24 B per sample slot) stay within
+  // kColourBytes; K = 32 for 1920x1080.
+  const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
+  const uint32_t spp = p->samples_per_pixel;
+  const uint32_t K = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp, kColourBytes / (24ull * nps)));
+  auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t elem) -> int {
+    if (need <= cap) return YK_OK;
+    (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    YK_HIP(hipMalloc((void**)&ptr, need * elem));
+    cap = need;
+    return YK_OK;
+  };
+  if ((rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)nps * K, sizeof(uint32_t)))) return rc;
+  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)nps * K * 3, sizeof(double)))) return rc;
+  if (spp > K && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
   ka.W = p->image_width;
@@ -855,8 +912,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.leaf_ids = ctx->d_leaf_ids;
   ka.geo = ctx->d_geo;
   ka.mat = ctx->d_mat;
-  ka.rgb = rgb_dev;
-  ka.sums = sums_dev;
+  ka.col = ctx->d_col;
   ka.pixel_counter = ctx->d_counter;
   ka.mt_scratch = ctx->d_mt;
   ka.id_scratch = ctx->d_ids;
@@ -868,23 +924,35 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.row_begin = p->row_begin;
   wa.row_stride = p->row_stride;
   wa.out = ctx->d_warm;
-  wa.pix_total = npix_total;
+  wa.npix_slots = nps;
   wa.pad = 0;
   wa.order = ctx->d_order;
-  ka.pix_total = npix_total;
+  ka.npix_slots = nps;
+  ka.pad_s = 0;
+  ka.pad_n = 0;
+  ReduceArgs ra;
+  ra.col = ctx->d_col;
+  ra.acc = ctx->d_acc;
+  ra.order = ctx->d_order;
+  ra.rgb = rgb_dev;
+  ra.sums = sums_dev;
+  ra.npix_slots = nps;
+  ra.spp = spp;
+  ra.pad0 = ra.pad1 = 0;
   YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
   YK_HIP(hipMemsetAsync(ctx->d_stats + 16, 0xff, 2 * sizeof(unsigned long long), st));  // minima
   YK_HIP(hipEventRecord(ctx->ev0, st));
   uint32_t launches = 0;
-  for (uint32_t p0 = 0; p0 < npix_total; p0 += chunk_pix) {
-    const uint32_t cnt = std::min(chunk_pix, npix_total - p0);
-    wa.pix_base = p0;
-    wa.n = (uint64_t)cnt * p->samples_per_pixel;
+  for (uint32_t s0 = 0; s0 < spp; s0 += K) {
+    const uint32_t ks = std::min(K, spp - s0);
+    const uint32_t nsl = nps * ks;
+    wa.s0 = s0;
+    wa.n = nsl;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * 32);
     hipLaunchKernelGGL(yk_mt_warmup, dim3(wblocks), dim3(256), 0, st, wa);
     YK_HIP(hipGetLastError());
-    ka.pix_base = p0;
-    ka.npix = cnt;
+    ka.s0 = s0;
+    ka.nsl = nsl;
     YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (ctx->scene_in_lds && count)
@@ -895,6 +963,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       hipLaunchKernelGGL((yk_render_persistent<false, true>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
     else
       hipLaunchKernelGGL((yk_render_persistent<false, false>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+    YK_HIP(hipGetLastError());
+    ra.nsl = nsl;
+    ra.ks = ks;
+    ra.first = s0 == 0;
+    ra.last = s0 + ks == spp;
+    hipLaunchKernelGGL(yk_reduce_samples, dim3((nps + 255) / 256), dim3(256), 0, st, ra);
     YK_HIP(hipGetLastError());
     ++launches;
   }
@@ -988,6 +1062,8 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_stats);
   (void)hipFree(ctx->d_warm);
   (void)hipFree(ctx->d_order);
+  (void)hipFree(ctx->d_col);
+  (void)hipFree(ctx->d_acc);
   (void)hipFree(ctx->d_nodes);
   (void)hipFree(ctx->d_leaf_geo);
   (void)hipFree(ctx->d_leaf_ids);
