@@ -758,7 +758,10 @@ struct ykgpu_context {
   uint32_t order_w = 0, order_rows = 0, order_slots = 0;
   size_t warm_cap = 0;
   hipStream_t stream = nullptr;
+  hipStream_t aux = nullptr;  // the MT warm-up of the next launches runs here, beside the render
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> lev;  // per launch: warm-up start, render start, reduce start, end
+  uint32_t lev_used = 0;
   SphereGeo* d_geo = nullptr;
   SphereMat* d_mat = nullptr;
   uint32_t nspheres = 0;
@@ -825,6 +828,12 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
 }
 
 constexpr uint64_t kColourBytes = 3ull << 29;  // 1.5 GiB of sample colours per launch at most
+// x_397 buffers: the warm-ups run on ctx->aux, beside the render launches (their wave slots and
+// VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots idle), into
+// a ring of min(launches, kWarmBytes / slot) slots, at least 3; warm-up c waits for the render of
+// launch c - ring.  With the whole call in the ring (1920x1080x512: 4.25 GB) every warm-up is
+// queued at once and none waits for a render to end.
+constexpr uint64_t kWarmBytes = 8ull << 30;
 #ifndef YK_TILE
 #define YK_TILE 8
 #endif
@@ -879,7 +888,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     cap = need;
     return YK_OK;
   };
-  if ((rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)nps * K, sizeof(uint32_t)))) return rc;
+  const uint32_t nlaunch = (spp + K - 1) / K;
+  const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
+      nlaunch, std::max<uint64_t>(3, kWarmBytes / (4ull * nps * K)));
+  if ((rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K, sizeof(uint32_t)))) return rc;
   if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)nps * K * 3, sizeof(double)))) return rc;
   if (spp > K && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
@@ -942,18 +954,42 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
   YK_HIP(hipMemsetAsync(ctx->d_stats + 16, 0xff, 2 * sizeof(unsigned long long), st));  // minima
   YK_HIP(hipEventRecord(ctx->ev0, st));
-  uint32_t launches = 0;
-  for (uint32_t s0 = 0; s0 < spp; s0 += K) {
-    const uint32_t ks = std::min(K, spp - s0);
-    const uint32_t nsl = nps * ks;
+  YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->ev0, 0));  // the caller's earlier work comes first
+  // per launch: [0] warm-up start, [1] warm-up end (aux), [2] render start, [3] render end,
+  // [4] reduce end (st)
+  while (ctx->lev.size() < 5ull * nlaunch) {
+    hipEvent_t e;
+    YK_HIP(hipEventCreate(&e));
+    ctx->lev.push_back(e);
+  }
+  ctx->lev_used = 5 * nlaunch;
+  auto warm = [&](uint32_t c) -> int {
+    hipEvent_t* ev = &ctx->lev[5 * c];
+    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[5 * (c - kWarmRing) + 3], 0));
+    const uint32_t s0 = c * K, ks = std::min(K, spp - s0);
     wa.s0 = s0;
-    wa.n = nsl;
+    wa.n = (uint64_t)nps * ks;
+    wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * 32);
-    hipLaunchKernelGGL(yk_mt_warmup, dim3(wblocks), dim3(256), 0, st, wa);
+    YK_HIP(hipEventRecord(ev[0], ctx->aux));
+    hipLaunchKernelGGL(yk_mt_warmup, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
     YK_HIP(hipGetLastError());
+    YK_HIP(hipEventRecord(ev[1], ctx->aux));
+    return YK_OK;
+  };
+  for (uint32_t c = 0; c < std::min(kWarmRing, nlaunch); ++c)
+    if ((rc = warm(c))) return rc;
+  uint32_t launches = 0;
+  for (uint32_t c = 0; c < nlaunch; ++c) {
+    hipEvent_t* ev = &ctx->lev[5 * c];
+    const uint32_t s0 = c * K, ks = std::min(K, spp - s0);
+    const uint32_t nsl = nps * ks;
     ka.s0 = s0;
     ka.nsl = nsl;
+    ka.warm = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
+    YK_HIP(hipStreamWaitEvent(st, ev[1], 0));
     YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
+    YK_HIP(hipEventRecord(ev[2], st));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (ctx->scene_in_lds && count)
       hipLaunchKernelGGL((yk_render_persistent<true, true>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
@@ -964,12 +1000,15 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     else
       hipLaunchKernelGGL((yk_render_persistent<false, false>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
     YK_HIP(hipGetLastError());
+    YK_HIP(hipEventRecord(ev[3], st));
     ra.nsl = nsl;
     ra.ks = ks;
     ra.first = s0 == 0;
     ra.last = s0 + ks == spp;
     hipLaunchKernelGGL(yk_reduce_samples, dim3((nps + 255) / 256), dim3(256), 0, st, ra);
     YK_HIP(hipGetLastError());
+    YK_HIP(hipEventRecord(ev[4], st));
+    if (c + kWarmRing < nlaunch && (rc = warm(c + kWarmRing))) return rc;
     ++launches;
   }
   YK_HIP(hipEventRecord(ctx->ev1, st));
@@ -994,7 +1033,19 @@ int finish_stats(ykgpu_context* ctx) {
   ctx->stats.newton_iters = c[7];
   for (int k = 0; k < 8; ++k) ctx->stats.phase_cycles[k] = c[8 + k];
   for (int k = 0; k < 3; ++k) ctx->stats.timeline[k] = c[16 + k];
-  ctx->stats.kernel_ms = ms;
+  ctx->stats.total_ms = ms;
+  double tw = 0, tr = 0, tp = 0;
+  for (uint32_t k = 0; k + 4 < ctx->lev_used; k += 5) {
+    float a = 0, b = 0, c = 0;
+    YK_HIP(hipEventSynchronize(ctx->lev[k + 1]));
+    YK_HIP(hipEventElapsedTime(&a, ctx->lev[k], ctx->lev[k + 1]));
+    YK_HIP(hipEventElapsedTime(&b, ctx->lev[k + 2], ctx->lev[k + 3]));
+    YK_HIP(hipEventElapsedTime(&c, ctx->lev[k + 3], ctx->lev[k + 4]));
+    tw += a, tr += b, tp += c;
+  }
+  ctx->stats.warmup_ms = tw;
+  ctx->stats.kernel_ms = tr;
+  ctx->stats.resolve_ms = tp;
   ctx->stats.segments = c[0];
   ctx->stats.sphere_tests = c[1];
   ctx->stats.sqrt_calls = c[2];
@@ -1042,6 +1093,7 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
                         (const void*)yk_render_persistent<true, true>, (const void*)yk_render_persistent<false, true>})
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_counter, 16) != hipSuccess ||
       hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
@@ -1071,9 +1123,11 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_ids);
   (void)hipFree(ctx->d_rgb);
   (void)hipFree(ctx->d_sums);
+  for (hipEvent_t e : ctx->lev) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   delete ctx;
   return YK_OK;
 }

@@ -86,6 +86,7 @@ class RenderStats(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("resolve_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double),
+        ("warmup_ms", ctypes.c_double),
         ("samples", ctypes.c_uint64),
         ("segments", ctypes.c_uint64),
         ("sphere_tests", ctypes.c_uint64),
