@@ -50,7 +50,7 @@ def pmc_facts(workload=None):
         rec = json.load(f)
     if workload is not None and rec.get("workload") != workload:
         return None
-    keep = ("source", "workload", "mean_ms", "valu_busy", "valu_lane_utilization",
+    keep = ("source", "kernel", "workload", "mean_ms", "valu_pipe_util", "valu_lane_utilization",
             "SQ_WAIT_ANY_frac", "SQ_WAIT_INST_ANY_frac", "hbm_bytes_per_launch",
             "fp64_flops_hw_per_launch")
     return {k: rec[k] for k in keep if k in rec}
@@ -145,7 +145,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    call_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    tst = ren.stats()  # per-kernel event timings of the last timed step (same stream)
+    kernel_ms = tst["kernel_ms"]  # the render kernel, summed over its launches in one step
+    launches = max(1, tst["launches"])
     # work counters: one more launch of the same workload with the counting instance, after the
     # timed region (the work is deterministic, so its counts are the timed launches' counts)
     ren.render_async(make_params(W, H, spp, depth, args.seed0, rows=rows, flags=1),
@@ -155,11 +158,15 @@ def main():
     total_samples = W * H * spp
     value = total_samples * args.steps / elapsed / 1e6
 
-    # roofline of the dominant kernel (this rank's launch): algorithmic FP64 work of the
-    # reference arithmetic actually executed, from the kernel's own unit counters
+    # roofline of the dominant kernel (yk_render_persistent, `launches` launches per step):
+    # algorithmic FP64 flops of the arithmetic it executed per launch (its own unit counters,
+    # / launches) over its average launch duration (HIP events around each launch)
     flops = fp64_flops(st)
-    achieved_tf = flops / (kernel_ms * 1e-3) / 1e12
-    hbm_bytes = rows_mine * W * 3 + len(spheres) * 96  # RGB8 out + scene in (algorithmic)
+    launch_ms = kernel_ms / launches
+    achieved_tf = (flops / launches) / (launch_ms * 1e-3) / 1e12
+    # algorithmic HBM bytes of the render kernel per step: x_397 in (4 B) + colour out (24 B)
+    # per sample, the scene once per launch
+    hbm_bytes = rows_mine * W * spp * (4 + 24) + launches * len(spheres) * 96
     workload = f"{args.scene}{args.scene_seed}_{W}x{H}x{spp}_d{depth}_n{world}"
     facts = pmc_facts(workload)
     traffic = facts.get("hbm_bytes_per_launch") if facts else None
@@ -191,18 +198,23 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 4),
             "traffic": traffic,
-            "kernel_ms": round(kernel_ms, 3),
-            "algorithmic": (f"FP64 flops of the reference arithmetic executed per launch = "
+            "kernel": "yk_render_persistent",
+            "launches_per_step": launches,
+            "avg_launch_ms": round(launch_ms, 3),
+            "step_breakdown_ms": {"render": round(kernel_ms, 3), "mt_warmup": round(tst["warmup_ms"], 3),
+                                  "reduce": round(tst["resolve_ms"], 3), "call": round(call_ms, 3)},
+            "algorithmic": (f"FP64 flops of the reference arithmetic executed per step = "
                             f"{FLOPS_PER_SPHERE_TEST}/sphere test x {st['sphere_tests']} + "
                             f"{FLOPS_PER_ROOT}/exact root x {st['sqrt_calls']} + math::sqrt "
                             f"(1/call x {st['newton_calls']} + {FLOPS_PER_NEWTON_ITER}/iteration x "
                             f"{st['newton_iters']}) + {FLOPS_PER_SEGMENT}/segment x "
                             f"{st['segments']} + {FLOPS_PER_SAMPLE}/sample x {st['samples']} = "
-                            f"{flops:.4g}"),
+                            f"{flops:.4g}, / {launches} launches"),
             "pmc": facts,
             "hbm": {"achieved_gbps": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 4),
                     "peak_gbps": HBM_PEAK_GBPS,
-                    "frac": hbm_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS},
+                    "frac": hbm_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                    "note": "algorithmic bytes: x_397 in + sample colour out (28 B/sample) + scene"},
             "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
             "tests_per_segment": round(st["sphere_tests"] / max(1, st["segments"]), 2),
         },
