@@ -827,7 +827,10 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
   return YK_OK;
 }
 
-constexpr uint64_t kColourBytes = 3ull << 29;  // 1.5 GiB of sample colours per launch at most
+#ifndef YK_COLOUR_MB
+#define YK_COLOUR_MB 3072
+#endif
+constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colours per launch at most
 // x_397 buffers: the warm-ups run on ctx->aux, beside the render launches (their wave slots and
 // VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots idle), into
 // a ring of min(launches, kWarmBytes / slot) slots, at least 3; warm-up c waits for the render of
@@ -875,10 +878,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   rc = ensure_order(ctx, p->image_width, p->row_count);
   if (rc) return rc;
   // Launches of K samples per pixel: the colours of a launch (24 B per sample slot) stay within
-  // kColourBytes; K = 32 for 1920x1080.
+  // kColourBytes, balanced over the launches (1920x1080x512: 8 launches of 64).  Each launch
+  // ends with the tail of its longest paths (~1 ms), so fewer, larger launches are better until
+  // the first warm-up, which the first render waits for, grows.
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
   const uint32_t spp = p->samples_per_pixel;
-  const uint32_t K = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp, kColourBytes / (24ull * nps)));
+  const uint32_t kmax = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp, kColourBytes / (24ull * nps)));
+  const uint32_t K = (spp + (spp + kmax - 1) / kmax - 1) / ((spp + kmax - 1) / kmax);
   auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t elem) -> int {
     if (need <= cap) return YK_OK;
     (void)hipFree(ptr);
