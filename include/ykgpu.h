@@ -106,9 +106,12 @@ typedef struct yk_render_params {
 } yk_render_params;
 
 typedef struct yk_render_stats {
-  double kernel_ms;        /* path-tracing kernel(s), HIP events on the render stream  */
-  double resolve_ms;       /* per-pixel sum + to_color3b kernel                        */
-  double total_ms;         /* whole call, host wall clock                              */
+  double kernel_ms;        /* path-tracing kernel, summed over its launches (HIP events on
+                              the render stream around each launch)                     */
+  double resolve_ms;       /* ordered per-pixel sum + to_color3b kernel, summed           */
+  double total_ms;         /* whole call: host wall clock for ykgpu_render / _sums (with
+                              the copies), first to last event for ykgpu_render_async   */
+  double warmup_ms;        /* MT seed-walk kernel, summed over its launches             */
   uint64_t samples;        /* primary samples rendered                                 */
   uint64_t segments;       /* ray_color calls that ran a closest-hit (flag COUNT_WORK) */
   uint64_t sphere_tests;   /* ray-sphere discriminant tests (flag COUNT_WORK)          */
