@@ -758,7 +758,8 @@ struct ykgpu_context {
   uint32_t order_w = 0, order_rows = 0, order_slots = 0;
   size_t warm_cap = 0;
   hipStream_t stream = nullptr;
-  hipStream_t aux = nullptr;  // the MT warm-up of the next launches runs here, beside the render
+  hipStream_t aux = nullptr;  // the MT warm-ups run here, beside the render launches
+  hipStream_t red = nullptr;  // the ordered reduces run here, beside the next render launch
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> lev;  // per launch: warm-up start, render start, reduce start, end
   uint32_t lev_used = 0;
@@ -837,6 +838,7 @@ constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colou
 // launch c - ring.  With the whole call in the ring (1920x1080x512: 4.25 GB) every warm-up is
 // queued at once and none waits for a render to end.
 constexpr uint64_t kWarmBytes = 8ull << 30;
+constexpr uint32_t kFirstLaunch = 8;  // samples per pixel in the first launch
 #ifndef YK_TILE
 #define YK_TILE 8
 #endif
@@ -884,7 +886,15 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
   const uint32_t spp = p->samples_per_pixel;
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp, kColourBytes / (24ull * nps)));
-  const uint32_t K = (spp + (spp + kmax - 1) / kmax - 1) / ((spp + kmax - 1) / kmax);
+  // schedule: a short first launch (the first render waits for its warm-up; the others' warm-ups
+  // run beside earlier renders), then launches of K balanced over the rest
+  const uint32_t k0 = spp > kmax ? std::min(kFirstLaunch, kmax) : spp;
+  std::vector<std::pair<uint32_t, uint32_t>> sched{{0u, k0}};  // (s0, samples)
+  if (spp > k0) {
+    const uint32_t rest = spp - k0, nr = (rest + kmax - 1) / kmax, kr = (rest + nr - 1) / nr;
+    for (uint32_t s0 = k0; s0 < spp; s0 += kr) sched.emplace_back(s0, std::min(kr, spp - s0));
+  }
+  const uint32_t K = std::max(k0, sched.size() > 1 ? sched[1].second : 0u);  // largest launch
   auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t elem) -> int {
     if (need <= cap) return YK_OK;
     (void)hipFree(ptr);
@@ -894,11 +904,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     cap = need;
     return YK_OK;
   };
-  const uint32_t nlaunch = (spp + K - 1) / K;
+  const uint32_t nlaunch = (uint32_t)sched.size();
   const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (4ull * nps * K)));
   if ((rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K, sizeof(uint32_t)))) return rc;
-  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)nps * K * 3, sizeof(double)))) return rc;
+  // two colour buffers: reduce c (stream red) overlaps render c + 1
+  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)2 * nps * K * 3, sizeof(double)))) return rc;
   if (spp > K && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
@@ -930,7 +941,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.leaf_ids = ctx->d_leaf_ids;
   ka.geo = ctx->d_geo;
   ka.mat = ctx->d_mat;
-  ka.col = ctx->d_col;
   ka.pixel_counter = ctx->d_counter;
   ka.mt_scratch = ctx->d_mt;
   ka.id_scratch = ctx->d_ids;
@@ -949,7 +959,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.pad_s = 0;
   ka.pad_n = 0;
   ReduceArgs ra;
-  ra.col = ctx->d_col;
   ra.acc = ctx->d_acc;
   ra.order = ctx->d_order;
   ra.rgb = rgb_dev;
@@ -961,20 +970,20 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   YK_HIP(hipMemsetAsync(ctx->d_stats + 16, 0xff, 2 * sizeof(unsigned long long), st));  // minima
   YK_HIP(hipEventRecord(ctx->ev0, st));
   YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->ev0, 0));  // the caller's earlier work comes first
-  // per launch: [0] warm-up start, [1] warm-up end (aux), [2] render start, [3] render end,
-  // [4] reduce end (st)
-  while (ctx->lev.size() < 5ull * nlaunch) {
+  // per launch: [0] warm-up start, [1] warm-up end (aux), [2] render start, [3] render end (st),
+  // [4] reduce start, [5] reduce end (red)
+  while (ctx->lev.size() < 6ull * nlaunch) {
     hipEvent_t e;
     YK_HIP(hipEventCreate(&e));
     ctx->lev.push_back(e);
   }
-  ctx->lev_used = 5 * nlaunch;
+  ctx->lev_used = 6 * nlaunch;
+  YK_HIP(hipStreamWaitEvent(ctx->red, ctx->ev0, 0));
   auto warm = [&](uint32_t c) -> int {
-    hipEvent_t* ev = &ctx->lev[5 * c];
-    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[5 * (c - kWarmRing) + 3], 0));
-    const uint32_t s0 = c * K, ks = std::min(K, spp - s0);
-    wa.s0 = s0;
-    wa.n = (uint64_t)nps * ks;
+    hipEvent_t* ev = &ctx->lev[6 * c];
+    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
+    wa.s0 = sched[c].first;
+    wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * 32);
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
@@ -987,13 +996,16 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     if ((rc = warm(c))) return rc;
   uint32_t launches = 0;
   for (uint32_t c = 0; c < nlaunch; ++c) {
-    hipEvent_t* ev = &ctx->lev[5 * c];
-    const uint32_t s0 = c * K, ks = std::min(K, spp - s0);
+    hipEvent_t* ev = &ctx->lev[6 * c];
+    const uint32_t s0 = sched[c].first, ks = sched[c].second;
     const uint32_t nsl = nps * ks;
+    double* col = ctx->d_col + (size_t)(c % 2) * nps * K * 3;
     ka.s0 = s0;
     ka.nsl = nsl;
+    ka.col = col;
     ka.warm = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
-    YK_HIP(hipStreamWaitEvent(st, ev[1], 0));
+    YK_HIP(hipStreamWaitEvent(st, ev[1], 0));                                // its x_397
+    if (c >= 2) YK_HIP(hipStreamWaitEvent(st, ctx->lev[6 * (c - 2) + 5], 0));  // its colour buffer
     YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
     YK_HIP(hipEventRecord(ev[2], st));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
@@ -1007,16 +1019,20 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       hipLaunchKernelGGL((yk_render_persistent<false, false>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[3], st));
+    ra.col = col;
     ra.nsl = nsl;
     ra.ks = ks;
     ra.first = s0 == 0;
     ra.last = s0 + ks == spp;
-    hipLaunchKernelGGL(yk_reduce_samples, dim3((nps + 255) / 256), dim3(256), 0, st, ra);
+    YK_HIP(hipStreamWaitEvent(ctx->red, ev[3], 0));
+    YK_HIP(hipEventRecord(ev[4], ctx->red));
+    hipLaunchKernelGGL(yk_reduce_samples, dim3((nps + 255) / 256), dim3(256), 0, ctx->red, ra);
     YK_HIP(hipGetLastError());
-    YK_HIP(hipEventRecord(ev[4], st));
+    YK_HIP(hipEventRecord(ev[5], ctx->red));
     if (c + kWarmRing < nlaunch && (rc = warm(c + kWarmRing))) return rc;
     ++launches;
   }
+  YK_HIP(hipStreamWaitEvent(st, ctx->lev[6 * (nlaunch - 1) + 5], 0));  // the caller sees the image
   YK_HIP(hipEventRecord(ctx->ev1, st));
   ctx->stats = yk_render_stats{};
   ctx->stats.samples = (uint64_t)p->row_count * p->image_width * p->samples_per_pixel;
@@ -1041,12 +1057,12 @@ int finish_stats(ykgpu_context* ctx) {
   for (int k = 0; k < 3; ++k) ctx->stats.timeline[k] = c[16 + k];
   ctx->stats.total_ms = ms;
   double tw = 0, tr = 0, tp = 0;
-  for (uint32_t k = 0; k + 4 < ctx->lev_used; k += 5) {
+  for (uint32_t k = 0; k + 5 < ctx->lev_used; k += 6) {
     float a = 0, b = 0, c = 0;
-    YK_HIP(hipEventSynchronize(ctx->lev[k + 1]));
+    YK_HIP(hipEventSynchronize(ctx->lev[k + 5]));
     YK_HIP(hipEventElapsedTime(&a, ctx->lev[k], ctx->lev[k + 1]));
     YK_HIP(hipEventElapsedTime(&b, ctx->lev[k + 2], ctx->lev[k + 3]));
-    YK_HIP(hipEventElapsedTime(&c, ctx->lev[k + 3], ctx->lev[k + 4]));
+    YK_HIP(hipEventElapsedTime(&c, ctx->lev[k + 4], ctx->lev[k + 5]));
     tw += a, tr += b, tp += c;
   }
   ctx->stats.warmup_ms = tw;
@@ -1100,6 +1116,7 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_counter, 16) != hipSuccess ||
       hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
@@ -1134,6 +1151,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+  if (ctx->red) (void)hipStreamDestroy(ctx->red);
   delete ctx;
   return YK_OK;
 }
