@@ -98,6 +98,8 @@ constexpr int kCounters = 20;  // [16..18]: timeline (diagnostic builds)
 #endif
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
 constexpr uint32_t kClaim = 128;    // sample slots a wave claims per atomic
+#define YK_STR2(x) #x
+#define YK_STR(x) YK_STR2(x)
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 
 struct KernelArgs {
@@ -501,6 +503,10 @@ void yk_render_persistent(KernelArgs ka) {
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
+#ifdef YK_NOPPAD
+            // diagnostic: YK_NOPPAD extra VALU issue slots per node visit (results unchanged)
+            asm volatile(".rept " YK_STR(YK_NOPPAD) "\n\tv_nop\n\t.endr" ::: "memory");
+#endif
 #if YK_ABLATE & 8
             // wave-level iterations of the interior-node loop (diagnostic): the first active
             // lane counts
@@ -829,7 +835,7 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
 }
 
 #ifndef YK_COLOUR_MB
-#define YK_COLOUR_MB 3072
+#define YK_COLOUR_MB 8192
 #endif
 constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colours per launch at most
 // x_397 buffers: the warm-ups run on ctx->aux, beside the render launches (their wave slots and
@@ -879,22 +885,25 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   if (rc) return rc;
   rc = ensure_order(ctx, p->image_width, p->row_count);
   if (rc) return rc;
-  // Launches of K samples per pixel: the colours of a launch (24 B per sample slot) stay within
-  // kColourBytes, balanced over the launches (1920x1080x512: 8 launches of 64).  Each launch
-  // ends with the tail of its longest paths (~1 ms), so fewer, larger launches are better until
-  // the first warm-up, which the first render waits for, grows.
+  // Launch schedule (samples per pixel per launch): 8, 32, 128, ... growing x4 up to the colour
+  // budget (24 B per sample slot, kColourBytes per launch), the last one taking a small
+  // remainder with it.  The first render waits only for an 8-sample warm-up; every later
+  // warm-up is ~0.15x the render before it, so it finishes underneath; and each launch ends with
+  // the tail of its longest paths (~1 ms), so there are few launches (1920x1080x512: 8, 32, 128,
+  // 172, 172).  Independent of the image size, which matters for the per-rank tiles of N GPUs.
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
   const uint32_t spp = p->samples_per_pixel;
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp, kColourBytes / (24ull * nps)));
-  // schedule: a short first launch (the first render waits for its warm-up; the others' warm-ups
-  // run beside earlier renders), then launches of K balanced over the rest
-  const uint32_t k0 = spp > kmax ? std::min(kFirstLaunch, kmax) : spp;
-  std::vector<std::pair<uint32_t, uint32_t>> sched{{0u, k0}};  // (s0, samples)
-  if (spp > k0) {
-    const uint32_t rest = spp - k0, nr = (rest + kmax - 1) / kmax, kr = (rest + nr - 1) / nr;
-    for (uint32_t s0 = k0; s0 < spp; s0 += kr) sched.emplace_back(s0, std::min(kr, spp - s0));
+  std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
+  for (uint32_t s0 = 0, k = std::min(kFirstLaunch, kmax); s0 < spp;) {
+    uint32_t take = std::min(k, spp - s0);
+    if (spp - (s0 + take) < std::max(1u, take / 4) && spp - s0 <= kmax) take = spp - s0;
+    sched.emplace_back(s0, take);
+    s0 += take;
+    k = std::min(4 * k, kmax);
   }
-  const uint32_t K = std::max(k0, sched.size() > 1 ? sched[1].second : 0u);  // largest launch
+  uint32_t K = 0;  // largest launch
+  for (auto& l : sched) K = std::max(K, l.second);
   auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t elem) -> int {
     if (need <= cap) return YK_OK;
     (void)hipFree(ptr);
@@ -910,7 +919,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   if ((rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K, sizeof(uint32_t)))) return rc;
   // two colour buffers: reduce c (stream red) overlaps render c + 1
   if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)2 * nps * K * 3, sizeof(double)))) return rc;
-  if (spp > K && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
+  if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
   ka.W = p->image_width;
