@@ -172,6 +172,46 @@ def test_headline_geometry_full_size_rows(ren):
     assert got.tobytes() == want.tobytes()
 
 
+def test_config2_full_image_vs_oracle(ren):
+    """BASELINE config 2 at its own size: 800x450, 100 spp, max_depth 50, the 5-sphere
+    lambertian + metal + dielectric scene, whole image, bytes and float64 sums bit-exact."""
+    arr, cam = yk.build_scene("rtiow5", 0)
+    ren.set_scene(arr, cam)
+    p = make_params(800, 450, 100, 50, 404)
+    got = ren.render_sums(p)
+    rgb_o, want, _, _ = oracle_lib.render(arr, cam, p, nthreads=16, want_sums=True)
+    assert got.tobytes() == want.tobytes()
+    np.testing.assert_array_equal(ren.render(p), rgb_o)
+
+
+def test_config4_geometry_rows_vs_oracle(ren):
+    """BASELINE config 4 geometry on one GPU: 3840x2160, 1024 spp, the final scene; rows 1080
+    and 2159, and the row set rank 3 of 8 renders (rows 3, 11, ...) checked on its first rows."""
+    arr, cam = yk.build_scene("final", 42)
+    ren.set_scene(arr, cam)
+    p = make_params(3840, 2160, 1024, 50, 404, rows=(1080, 2, 1079))
+    got = ren.render_sums(p)
+    _, want, _, _ = oracle_lib.render(arr, cam, p, nthreads=16, want_rgb=False, want_sums=True)
+    assert got.tobytes() == want.tobytes()
+    tile = ren.render(make_params(3840, 2160, 64, 50, 404, rows=(3, 270, 8)))
+    ref, _, _, _ = oracle_lib.render(arr, cam, make_params(3840, 2160, 64, 50, 404, rows=(3, 2, 8)),
+                                     nthreads=16)
+    np.testing.assert_array_equal(tile[:2], ref)
+
+
+def test_config5_dielectric_rows_vs_oracle(ren):
+    """BASELINE config 5: 1920x1080, 4096 spp, max_depth 200, the dielectric-heavy scene (long,
+    divergent bounce chains; samples drawing past the lazy MT window); two rows bit-exact."""
+    arr, cam = yk.build_scene("glass", 42)
+    ren.set_scene(arr, cam)
+    p = make_params(1920, 1080, 4096, 200, 404, rows=(500, 2, 40))
+    got = ren.render_sums(p)
+    st = ren.stats()
+    _, want, _, _ = oracle_lib.render(arr, cam, p, nthreads=16, want_rgb=False, want_sums=True)
+    assert got.tobytes() == want.tobytes()
+    assert st["mt_fallbacks"] > 0  # the 624-word scratch engine was exercised
+
+
 def test_bad_rows_rejected(ren):
     ren.set_scene(refscenes.ref4(), refscenes.reference_camera())
     with pytest.raises(yk.YkError):
