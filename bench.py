@@ -95,11 +95,17 @@ def main():
     from uecraytracing_amd.records import image_height_for, make_params
     from uecraytracing_amd.tiles import TileGather, tile_rows
 
+    # one process per GPU; YK_BENCH_BACKEND=gloo (rehearsal only) lets several ranks share a GPU
+    backend = os.environ.get("YK_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     dev = torch.device("cuda", local)
 
     W, spp, depth = args.width, args.spp, args.depth

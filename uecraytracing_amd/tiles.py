@@ -48,7 +48,15 @@ class TileGather:
         if self.world == 1:
             self.image.copy_(self.tile[: self.height])
             return self.image
-        dist.gather(self.tile, list(self.gathered.unbind(0)) if self.rank == 0 else None, dst=0)
+        if self.tile.is_cuda and dist.get_backend() == "gloo":
+            # gloo gathers host tensors (test rehearsals of the N-rank path on one GPU)
+            cpu = self.tile.cpu()
+            outs = [torch.empty_like(cpu) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(cpu, outs, dst=0)
+            if self.rank == 0:
+                self.gathered.copy_(torch.stack(outs))
+        else:
+            dist.gather(self.tile, list(self.gathered.unbind(0)) if self.rank == 0 else None, dst=0)
         if self.rank == 0:
             torch.index_select(self.gathered.reshape(self.world * self.rm, self.width, 3), 0,
                                self.index, out=self.image)
