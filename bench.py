@@ -110,7 +110,14 @@ def main():
 
     W, spp, depth = args.width, args.spp, args.depth
     H = image_height_for(W)
-    spheres, cam = yk.build_scene(args.scene, args.scene_seed)
+    # the committed scene file of the config when there is one (identical to the seeded
+    # generator's output, tests/test_scene_files.py), else the generator
+    scene_file = os.path.join(yk.SCENE_DIR, f"{args.scene}_seed{args.scene_seed}.yks")
+    if os.path.exists(scene_file):
+        spheres, cam = yk.read_scene(scene_file)
+    else:
+        scene_file = None
+        spheres, cam = yk.build_scene(args.scene, args.scene_seed)
     rows = tile_rows(rank, world, H)
     rows_mine = rows[1]
     params = make_params(W, H, spp, depth, args.seed0, rows=rows, flags=0)  # production instance
@@ -195,6 +202,7 @@ def main():
                         f"scene ({len(spheres)} spheres, generator seed {args.scene_seed}), "
                         f"seed0 {args.seed0}, mt19937 + FP64 bit-exact",
             "image": f"{W}x{H}", "spp": spp, "max_depth": depth, "spheres": len(spheres),
+            "scene_file": os.path.relpath(scene_file, ROOT) if scene_file else None,
             "partition": f"cyclic rows over {world} GPU(s), RCCL gather to rank 0",
         },
         "roofline": {

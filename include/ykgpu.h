@@ -188,6 +188,14 @@ int yk_camera_look(yk_camera* out, const double lookfrom[3], const double lookat
 int yk_scene_build(const char* name, uint32_t seed, yk_sphere* spheres, uint32_t capacity,
                    uint32_t* count, yk_camera* camera);
 
+/* Scene files (an on-disk format for generated scenes).  Text: a "yk-scene 1"
+ * header, one "camera" line (origin, lower_left_corner, horizontal, vertical, lens_u, lens_v,
+ * lens_radius) and one "sphere <lambertian|metal|dielectric> cx cy cz radius r g b fuzz ior"
+ * line per sphere in tuple order; numbers as %.17g, so every double round-trips exactly.
+ * yk_scene_read follows yk_scene_build's capacity/count/camera convention. */
+int yk_scene_write(const char* path, const yk_sphere* spheres, uint32_t count, const yk_camera* camera);
+int yk_scene_read(const char* path, yk_sphere* spheres, uint32_t capacity, uint32_t* count, yk_camera* camera);
+
 /* Image height of the reference for a width: uint32(W / (16.0/9.0)) (source.cpp:61-62). */
 uint32_t yk_image_height_for(uint32_t width);
 

@@ -27,8 +27,9 @@ EXPORTS = (
     "ykgpu_abi_version", "ykgpu_last_error", "ykgpu_device_count", "ykgpu_context_create",
     "ykgpu_context_destroy", "ykgpu_set_scene", "ykgpu_render", "ykgpu_render_async",
     "ykgpu_render_sums", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_div", "yk_camera_reference", "yk_camera_look",
-    "yk_scene_build", "yk_image_height_for",
+    "yk_scene_build", "yk_scene_write", "yk_scene_read", "yk_image_height_for",
 )
+SCENE_DIR = os.path.join(PKG_DIR, "scenes")  # committed scene files of the BASELINE configs
 
 _lib = None
 
@@ -73,6 +74,8 @@ def load_library():
                             c.c_double, c.c_double, c.c_double], c.c_int),
         "yk_scene_build": ([c.c_char_p, c.c_uint32, P(Sphere), c.c_uint32, P(c.c_uint32),
                             P(Camera)], c.c_int),
+        "yk_scene_write": ([c.c_char_p, P(Sphere), c.c_uint32, P(Camera)], c.c_int),
+        "yk_scene_read": ([c.c_char_p, P(Sphere), c.c_uint32, P(c.c_uint32), P(Camera)], c.c_int),
         "yk_image_height_for": ([c.c_uint32], c.c_uint32),
     }
     for name, (args, res) in sig.items():
@@ -109,6 +112,22 @@ def build_scene(name: str, seed: int = 0):
     _check(lib.yk_scene_build(name.encode(), seed, None, 0, ctypes.byref(n), ctypes.byref(cam)))
     arr = (Sphere * n.value)()
     _check(lib.yk_scene_build(name.encode(), seed, arr, n.value, ctypes.byref(n), None))
+    return arr, cam
+
+
+def write_scene(path: str, spheres, camera: Camera):
+    """Scene file (include/ykgpu.h yk_scene_write): tuple order, exact doubles."""
+    arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
+    _check(load_library().yk_scene_write(os.fsencode(path), arr, len(arr), ctypes.byref(camera)))
+
+
+def read_scene(path: str):
+    """Returns (spheres ctypes array, Camera) from a scene file."""
+    lib = load_library()
+    n, cam = ctypes.c_uint32(0), Camera()
+    _check(lib.yk_scene_read(os.fsencode(path), None, 0, ctypes.byref(n), ctypes.byref(cam)))
+    arr = (Sphere * n.value)()
+    _check(lib.yk_scene_read(os.fsencode(path), arr, n.value, ctypes.byref(n), None))
     return arr, cam
 
 
@@ -181,5 +200,5 @@ class Renderer:
         return st.as_dict()
 
 
-__all__ = ["Renderer", "YkError", "build_scene", "reference_camera", "device_count",
+__all__ = ["Renderer", "YkError", "build_scene", "write_scene", "read_scene", "SCENE_DIR", "reference_camera", "device_count",
            "make_params", "load_library", "records", "EXPORTS", "LIB_PATH", "CLI_PATH"]

@@ -11,7 +11,7 @@
 // reference scene (source.cpp:103-112), built with the same yk calls.
 //
 // Added (render parameters are compile-time macros in the reference): --width, --spp,
-// --depth, --scene, --scene-seed, --seed0, --device, --stats.  --seed0 fixes the per-sample seed
+// --depth, --scene, --scene-seed, --scene-file, --save-scene, --seed0, --device, --stats.  --seed0 fixes the per-sample seed
 // base (seed0 + (y*W+x)*spp + s, source.cpp:154-158); without it seed0 comes from
 // std::random_device, like the reference's runtime build draws every sample's seed from it.
 // Verbose output: levels 1-2 print the reference's per-pixel / per-sample lines after the GPU
@@ -61,6 +61,8 @@ const char* kHelp =
     "      --depth arg           max bounce depth (default: 50)\n"
     "      --scene arg           ref4|lambert3|mixed12|walls2|rtiow5|final|glass (default: ref4)\n"
     "      --scene-seed arg      generator seed of final/glass (default: 42)\n"
+    "      --scene-file arg      load the scene from a yk-scene file (overrides --scene)\n"
+    "      --save-scene arg      write the scene to a yk-scene file\n"
     "      --seed0 arg           per-sample seed base (default: random_device)\n"
     "      --device arg          GPU index (default: 0)\n"
     "      --stats               print kernel time and throughput\n";
@@ -75,6 +77,7 @@ struct args {
   bool have_seed0 = false;
   uint32_t seed0 = 0;
   std::string scene = "ref4";
+  std::string scene_file, save_scene;
 };
 
 uint32_t to_u32(const std::string& opt, const std::string& v) {
@@ -121,6 +124,8 @@ args parse(int argc, char** argv) {
       else if (n == "scene-seed") a.scene_seed = to_u32(n, value(i, n, inl));
       else if (n == "device") a.device = (int)to_u32(n, value(i, n, inl));
       else if (n == "scene") a.scene = value(i, n, inl);
+      else if (n == "scene-file") a.scene_file = value(i, n, inl);
+      else if (n == "save-scene") a.save_scene = value(i, n, inl);
       else if (n == "seed0") { a.seed0 = to_u32(n, value(i, n, inl)); a.have_seed0 = true; }
       else throw option_error{"Option '" + n + "' does not exist"};
     } else if (s.size() > 1 && s[0] == '-') {
@@ -177,7 +182,18 @@ int main(int argc, char* argv[]) {
   std::vector<uint8_t> image;
   try {
     ykgpu::renderer gpu(a.device);
-    if (a.scene == "ref4") {
+    if (!a.scene_file.empty()) {
+      uint32_t n = 0;
+      yk_camera cam;
+      if (yk_scene_read(a.scene_file.c_str(), nullptr, 0, &n, &cam) != YK_OK) {
+        std::cerr << "cannot read scene file " << a.scene_file << std::endl;
+        return EXIT_FAILURE;
+      }
+      std::vector<yk_sphere> s(n);
+      yk_scene_read(a.scene_file.c_str(), s.data(), n, &n, nullptr);
+      gpu.set_records(s, cam);
+      if (!a.save_scene.empty()) yk_scene_write(a.save_scene.c_str(), s.data(), n, &cam);
+    } else if (a.scene == "ref4") {
       // the reference's world, built with the reference's calls (source.cpp:100-112)
       using T = double;
       using yk::lambertian, yk::metal, yk::pos3, yk::sphere, yk::world_tag;
@@ -189,6 +205,11 @@ int main(int argc, char* argv[]) {
               .add(sphere(pos3<T, world_tag>(-1.0, 0.0, -1.0), 0.5, metal<double>({0.8, 0.8, 0.8})))
               .add(sphere(pos3<T, world_tag>(1.0, 0.0, -1.0), 0.5, metal<double>({0.8, 0.6, 0.2})));
       gpu.set_scene(world, cam);
+      if (!a.save_scene.empty()) {
+        const std::vector<yk_sphere> s = ykgpu::flatten(world);
+        const yk_camera c = ykgpu::camera_record(cam);
+        yk_scene_write(a.save_scene.c_str(), s.data(), (uint32_t)s.size(), &c);
+      }
     } else {
       uint32_t n = 0;
       yk_camera cam;
@@ -199,6 +220,7 @@ int main(int argc, char* argv[]) {
       std::vector<yk_sphere> s(n);
       yk_scene_build(a.scene.c_str(), a.scene_seed, s.data(), n, &n, nullptr);
       gpu.set_records(s, cam);
+      if (!a.save_scene.empty()) yk_scene_write(a.save_scene.c_str(), s.data(), n, &cam);
     }
     std::cout << "rendering..." << std::endl;
     image = gpu.render(W, H, a.spp, a.depth, seed0);

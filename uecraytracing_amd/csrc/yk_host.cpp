@@ -2,6 +2,7 @@
 // the positionable camera extension and the named scenes of the BASELINE configs.
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -212,3 +213,89 @@ int yk_scene_build(const char* name, uint32_t seed, yk_sphere* spheres, uint32_t
 }
 
 }  // extern "C"
+
+// ---- scene files -------------------------------------------------------------------------
+// Text, one record per line, numbers as %.17g (every double round-trips exactly):
+//   yk-scene 1
+//   camera <origin 3> <lower_left_corner 3> <horizontal 3> <vertical 3> <lens_u 3> <lens_v 3> <lens_radius>
+//   sphere <lambertian|metal|dielectric> <cx cy cz> <radius> <albedo r g b> <fuzz> <ior>
+// '#' starts a comment line.  The spheres keep file order = tuple order (it defines rec.id).
+namespace {
+const char* kind_name(uint32_t k) {
+  return k == YK_MATERIAL_LAMBERTIAN ? "lambertian" : k == YK_MATERIAL_METAL ? "metal" : "dielectric";
+}
+}  // namespace
+
+int yk_scene_write(const char* path, const yk_sphere* spheres, uint32_t count, const yk_camera* camera) {
+  if (!path || !camera || (count && !spheres)) return YK_ERR_INVALID;
+  FILE* f = std::fopen(path, "w");
+  if (!f) return YK_ERR_INVALID;
+  std::fprintf(f, "yk-scene 1\n# %u spheres; tuple order\ncamera", count);
+  const double* cv[6] = {camera->origin, camera->lower_left_corner, camera->horizontal,
+                         camera->vertical, camera->lens_u, camera->lens_v};
+  for (const double* v : cv) std::fprintf(f, " %.17g %.17g %.17g", v[0], v[1], v[2]);
+  std::fprintf(f, " %.17g\n", camera->lens_radius);
+  for (uint32_t i = 0; i < count; ++i) {
+    const yk_sphere& s = spheres[i];
+    std::fprintf(f, "sphere %s %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", kind_name(s.material),
+                 s.center[0], s.center[1], s.center[2], s.radius, s.albedo[0], s.albedo[1], s.albedo[2],
+                 s.fuzz, s.ior);
+  }
+  const bool ok = std::ferror(f) == 0;
+  return (std::fclose(f) == 0 && ok) ? YK_OK : YK_ERR_INVALID;
+}
+
+int yk_scene_read(const char* path, yk_sphere* spheres, uint32_t capacity, uint32_t* count, yk_camera* camera) {
+  if (!path) return YK_ERR_INVALID;
+  FILE* f = std::fopen(path, "r");
+  if (!f) return YK_ERR_INVALID;
+  std::vector<yk_sphere> w;
+  yk_camera cam{};
+  bool have_header = false, have_camera = false, bad = false;
+  char line[1024];
+  while (!bad && std::fgets(line, sizeof line, f)) {
+    char word[32] = {0};
+    if (line[0] == '#' || std::sscanf(line, "%31s", word) != 1) continue;
+    const std::string wd = word;
+    if (wd == "yk-scene") {
+      int v = 0;
+      bad = std::sscanf(line, "%*s %d", &v) != 1 || v != 1;
+      have_header = true;
+    } else if (wd == "camera") {
+      double* cv[6] = {cam.origin, cam.lower_left_corner, cam.horizontal, cam.vertical, cam.lens_u, cam.lens_v};
+      const char* p = line + 6;
+      int used = 0;
+      for (double* v : cv)
+        for (int k = 0; k < 3 && !bad; ++k) {
+          bad = std::sscanf(p, "%lf%n", &v[k], &used) != 1;
+          p += used;
+        }
+      bad = bad || std::sscanf(p, "%lf", &cam.lens_radius) != 1;
+      have_camera = true;
+    } else if (wd == "sphere") {
+      yk_sphere s;
+      std::memset(&s, 0, sizeof s);
+      char kind[32] = {0};
+      bad = std::sscanf(line, "%*s %31s %lf %lf %lf %lf %lf %lf %lf %lf %lf", kind, &s.center[0], &s.center[1],
+                        &s.center[2], &s.radius, &s.albedo[0], &s.albedo[1], &s.albedo[2], &s.fuzz, &s.ior) != 10;
+      const std::string k = kind;
+      if (k == "lambertian") s.material = YK_MATERIAL_LAMBERTIAN;
+      else if (k == "metal") s.material = YK_MATERIAL_METAL;
+      else if (k == "dielectric") s.material = YK_MATERIAL_DIELECTRIC;
+      else bad = true;
+      w.push_back(s);
+    } else {
+      bad = true;
+    }
+  }
+  std::fclose(f);
+  if (bad || !have_header || !have_camera) return YK_ERR_INVALID;
+  if (count) *count = (uint32_t)w.size();
+  if (camera) *camera = cam;
+  if (spheres) {
+    if (capacity < w.size()) return YK_ERR_INVALID;
+    if (!w.empty()) std::memcpy(spheres, w.data(), w.size() * sizeof(yk_sphere));
+  }
+  return YK_OK;
+}
+
