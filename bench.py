@@ -260,6 +260,26 @@ def main():
                       f"{n} samples of the same workload, {dt:.1f} s, oracle/yk_oracle.c "
                       f"(-O2, {nthreads} threads)",
         }
+        # SURVEY §8(d) variants: the same port on ONE core (one row), and the reference's
+        # as-shipped cost model (a random_device seed per sample, source.cpp:159) on all threads
+        r1 = make_params(W, H, spp, depth, args.seed0, rows=(H // 2, 1, 1))
+        t = time.perf_counter()
+        oracle_lib.render(spheres, cam, r1, nthreads=1)
+        dt1 = time.perf_counter() - t
+        rows_as = list(range(0, H, args.cpu_row_step * 4))
+        ra = make_params(W, H, spp, depth, args.seed0, rows=(0, len(rows_as), args.cpu_row_step * 4))
+        t = time.perf_counter()
+        oracle_lib.render_as_shipped(spheres, cam, ra, nthreads=nthreads)
+        dta = time.perf_counter() - t
+        result["cpu_baseline"]["variants"] = {
+            "port_1_core": {"value": round(W * spp / dt1 / 1e6, 4), "cores": 1,
+                            "sample": f"row {H // 2} x {W} px x {spp} spp, {dt1:.1f} s"},
+            "as_shipped_cost_model": {
+                "value": round(len(rows_as) * W * spp / dta / 1e6, 4), "cores": nthreads,
+                "sample": f"{len(rows_as)} rows (every {args.cpu_row_step * 4}th) x {W} px x {spp} spp, "
+                          f"{dta:.1f} s; a random_device seed per sample as in the runtime build "
+                          f"(source.cpp:159), so not reproducible"},
+        }
         result["parity_vs_cpu"] = {
             "rows_compared": len(rows),
             "rmse": float(np.sqrt(np.mean(diff ** 2))),

@@ -17,7 +17,9 @@
  * -ffp-contract=off).  Citations are /root/reference/<file>:<line>.
  */
 #include <math.h>
+#include <fcntl.h>
 #include <pthread.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -136,6 +138,7 @@ typedef struct {
   const yk_camera* cam;
   const yk_render_params* p;
   uint64_t tests; /* ray-sphere tests (diagnostics) */
+  int as_shipped; /* seed every sample from /dev/urandom like the runtime build (timing only) */
 } world_t;
 
 typedef struct {
@@ -264,13 +267,29 @@ static c3 ray_color(world_t* w, v3 o, v3 d, uint32_t depth, mt_t* g, uint64_t* s
   return r;
 }
 
+/* The runtime build's seed, source.cpp:159: a std::random_device constructed per sample.
+ * libstdc++'s random_device opens its entropy source, reads one word and closes it again; this
+ * models that cost with /dev/urandom (timing of the as-shipped cost model only: the image is not
+ * reproducible, as in the reference). */
+static uint32_t random_device_u32(void) {
+  uint32_t v = 0;
+  int fd = open("/dev/urandom", O_RDONLY);
+  if (fd >= 0) {
+    if (read(fd, &v, sizeof v) != (ssize_t)sizeof v) v = 0;
+    close(fd);
+  }
+  return v;
+}
+
 /* One sample: source.cpp:154-166 (seed :154-158, jitter :160-164, get_ray camera.hpp:29-32
  * or the thin-lens extension). */
 static c3 sample(world_t* w, uint32_t y, uint32_t x, uint32_t s, uint64_t* draws, uint64_t* segs) {
   const yk_render_params* p = w->p;
   const yk_camera* cam = w->cam;
   mt_t g;
-  mt_seed(&g, p->seed0 + (y * p->image_width + x) * p->samples_per_pixel + s);
+  uint32_t seed = p->seed0 + (y * p->image_width + x) * p->samples_per_pixel + s;
+  if (w->as_shipped) seed = random_device_u32();
+  mt_seed(&g, seed);
   double u = (x + mt_uniform(&g, 0, 1)) / p->image_width;
   double v = (p->image_height - y - 1 + mt_uniform(&g, 0, 1)) / p->image_height;
   v3 org = v3_of(cam->origin);
@@ -326,11 +345,12 @@ typedef struct {
   double* sums;
   uint32_t tid, nthreads;
   uint64_t segs, tests;
+  int as_shipped;
 } job_t;
 
 static void* worker(void* arg) {
   job_t* j = (job_t*)arg;
-  world_t w = {j->s, j->n, j->cam, j->p, 0};
+  world_t w = {j->s, j->n, j->cam, j->p, 0, j->as_shipped};
   const uint32_t W = j->p->image_width;
   for (uint32_t i = j->tid; i < j->p->row_count; i += j->nthreads) {
     uint32_t y = j->p->row_begin + i * j->p->row_stride;
@@ -364,8 +384,9 @@ static int check(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_
 /* Render the rows named by p into rgb (row_count*W*3 bytes) and/or sums (row_count*W*3
  * doubles), with `nthreads` host threads over interleaved rows.  Returns YK_* status;
  * *segments / *tests (nullable) receive work counts. */
-int yko_render(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p,
-               uint8_t* rgb, double* sums, int nthreads, uint64_t* segments, uint64_t* tests) {
+static int render_impl(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p,
+                       uint8_t* rgb, double* sums, int nthreads, uint64_t* segments, uint64_t* tests,
+                       int as_shipped) {
   int st = check(s, n, cam, p);
   if (st) return st;
   if (nthreads < 1) nthreads = 1;
@@ -374,7 +395,7 @@ int yko_render(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_re
   pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
   if (!jobs || !th) { free(jobs); free(th); return YK_ERR_NOMEM; }
   for (int t = 0; t < nthreads; ++t) {
-    job_t jj = {s, n, cam, p, rgb, sums, (uint32_t)t, (uint32_t)nthreads, 0, 0};
+    job_t jj = {s, n, cam, p, rgb, sums, (uint32_t)t, (uint32_t)nthreads, 0, 0, as_shipped};
     jobs[t] = jj;
   }
   for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], 0, worker, &jobs[t]);
@@ -392,12 +413,24 @@ int yko_render(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_re
   return YK_OK;
 }
 
+int yko_render(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p,
+               uint8_t* rgb, double* sums, int nthreads, uint64_t* segments, uint64_t* tests) {
+  return render_impl(s, n, cam, p, rgb, sums, nthreads, segments, tests, 0);
+}
+
+/* The same loop with the runtime build's per-sample random_device seeding (source.cpp:159): the
+ * reference's as-shipped cost model for the CPU baseline (SURVEY §8(d) variant i).  Timing only. */
+int yko_render_as_shipped(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p,
+                          uint8_t* rgb, double* sums, int nthreads, uint64_t* segments, uint64_t* tests) {
+  return render_impl(s, n, cam, p, rgb, sums, nthreads, segments, tests, 1);
+}
+
 /* One sample's colour and its u32 draw count (per-sample path fixtures). */
 int yko_sample(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p,
                uint32_t y, uint32_t x, uint32_t smp, double* rgb3, uint64_t* draws) {
   int st = check(s, n, cam, p);
   if (st) return st;
-  world_t w = {s, n, cam, p, 0};
+  world_t w = {s, n, cam, p, 0, 0};
   c3 c = sample(&w, y, x, smp, draws, 0);
   rgb3[0] = c.r; rgb3[1] = c.g; rgb3[2] = c.b;
   return YK_OK;

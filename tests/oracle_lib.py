@@ -31,6 +31,8 @@ def load():
                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                P(ctypes.c_uint64), P(ctypes.c_uint64)]
     lib.yko_render.restype = ctypes.c_int
+    lib.yko_render_as_shipped.argtypes = lib.yko_render.argtypes
+    lib.yko_render_as_shipped.restype = ctypes.c_int
     lib.yko_sample.argtypes = [P(Sphere), ctypes.c_uint32, P(Camera), P(RenderParams),
                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                P(ctypes.c_double), P(ctypes.c_uint64)]
@@ -64,6 +66,21 @@ def render(spheres, camera: Camera, params: RenderParams, nthreads=None, want_rg
     if st != 0:
         raise RuntimeError(f"oracle render failed: {st}")
     return rgb, sums, segs.value, tests.value
+
+
+def render_as_shipped(spheres, camera: Camera, params: RenderParams, nthreads=None):
+    """The reference's as-shipped cost model (per-sample random_device seeding): timing only,
+    the image is not reproducible.  Returns segments."""
+    lib = load()
+    arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
+    rgb = np.zeros((params.row_count, params.image_width, 3), np.uint8)
+    segs, tests = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    nt = nthreads or max(1, min(os.cpu_count() or 1, 8))
+    st = lib.yko_render_as_shipped(arr, len(arr), ctypes.byref(camera), ctypes.byref(params),
+                                   rgb.ctypes.data, None, nt, ctypes.byref(segs), ctypes.byref(tests))
+    if st != 0:
+        raise RuntimeError(f"oracle render failed: {st}")
+    return segs.value
 
 
 def sample(spheres, camera, params, y, x, s):
