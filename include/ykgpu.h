@@ -127,6 +127,7 @@ typedef struct yk_render_stats {
   uint64_t timeline[3];    /* diagnostic builds only: s_memrealtime (100 MHz) of the first wave start, of
                               the first refill that found no pixel left, of the last wave
                               exit (last launch of the call)                              */
+  uint64_t diag[4];        /* diagnostic builds only: [0] leaf tests with disc >= 0       */
   uint32_t launches;       /* path-tracing launches in the call                        */
   uint32_t grid_blocks;    /* persistent grid size                                     */
 } yk_render_stats;

@@ -21,8 +21,10 @@ with yk.Renderer(0) as r:
         span = tl[2] - tl[0]
         print(f"timeline: pixels exhausted at {(tl[1] - tl[0]) / span * 100:.1f}% of the launch "
               f"({span / 1e5:.1f} ms), tail {(tl[2] - tl[1]) / span * 100:.1f}%")
+    diag = st["diag"]
     r.render(make_params(1920, None, spp, 50, 404, flags=1))
     st2 = r.stats()
+    print(f"leaf tests {st2['sphere_tests']}, with disc >= 0 {diag[0]} ({diag[0] / max(1, st2['sphere_tests']):.3f})")
     print(f"node visits (lanes) {st2['node_visits']}, wave-level node-loop iterations {node_iters} -> "
           f"lane utilisation in the node loop {st2['node_visits'] / max(1, node_iters * 64):.3f}; "
           f"wave-cycles per node iteration {pc[2] / max(1, node_iters):.0f}")

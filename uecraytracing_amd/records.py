@@ -98,6 +98,7 @@ class RenderStats(ctypes.Structure):
         ("newton_iters", ctypes.c_uint64),
         ("phase_cycles", ctypes.c_uint64 * 8),
         ("timeline", ctypes.c_uint64 * 3),
+        ("diag", ctypes.c_uint64 * 4),
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
     ]
@@ -106,6 +107,7 @@ class RenderStats(ctypes.Structure):
         d = {f: getattr(self, f) for f, _ in self._fields_}
         d["phase_cycles"] = list(self.phase_cycles)
         d["timeline"] = list(self.timeline)
+        d["diag"] = list(self.diag)
         return d
 
 
