@@ -76,7 +76,7 @@ static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 #define YK_WAVES_PER_EU 0
 #endif
 constexpr int kBlock = YK_BLOCK;
-constexpr int kCounters = 20;  // [16..18]: timeline (diagnostic builds)
+constexpr int kCounters = 24;  // [16..18]: timeline, [19..22]: diag (diagnostic builds)
 
 // Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
 // points, summed per phase into counters[8..13] (refill, start, traversal, candidates, shade,
@@ -357,6 +357,7 @@ void yk_render_persistent(KernelArgs ka) {
 
 #if YK_ABLATE & 8
   uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_diag0 = 0;  // leaf tests with disc >= 0
   uint64_t st_prev = __builtin_amdgcn_s_memtime();
   if (lane == 0) atomicMin(&ka.counters[16], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
@@ -554,6 +555,9 @@ void yk_render_persistent(KernelArgs ka) {
               const double c = ykd::len2(oc) - sg.rr;
               const double disc = hb * hb - a * c;
               if (disc < 0) continue;
+#if YK_ABLATE & 8
+              ++st_diag0;
+#endif
               // bounds of the exact root: |approx - exact| <= m (256x the error bound, §4)
               const double sq = ykd::sqrt_bound(disc);
               const double r1 = (-hb - sq) * ia, r2 = (-hb + sq) * ia;
@@ -729,6 +733,7 @@ void yk_render_persistent(KernelArgs ka) {
   if (lane == 0)
     for (int k = 0; k < 7; ++k) atomicAdd(&ka.counters[8 + k], (unsigned long long)st_acc[k]);
   atomicAdd(&ka.counters[15], (unsigned long long)st_acc[7]);  // per-lane partial counts
+  atomicAdd(&ka.counters[19], (unsigned long long)st_diag0);
   if (lane == 0) atomicMax(&ka.counters[18], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
   if (kCount) {
@@ -1064,6 +1069,7 @@ int finish_stats(ykgpu_context* ctx) {
   ctx->stats.newton_iters = c[7];
   for (int k = 0; k < 8; ++k) ctx->stats.phase_cycles[k] = c[8 + k];
   for (int k = 0; k < 3; ++k) ctx->stats.timeline[k] = c[16 + k];
+  for (int k = 0; k < 4; ++k) ctx->stats.diag[k] = c[19 + k];
   ctx->stats.total_ms = ms;
   double tw = 0, tr = 0, tp = 0;
   for (uint32_t k = 0; k + 5 < ctx->lev_used; k += 6) {
