@@ -141,6 +141,14 @@ inline void check(int rc, const char* where) {
   if (rc != YK_OK) throw error(rc, std::string(where) + ": " + ykgpu_last_error());
 }
 
+// The non-default yk_render_params modes (include/ykgpu.h).
+struct render_options {
+  uint32_t precision = YK_PRECISION_FP64;  // YK_PRECISION_FP32: render<float>
+  uint32_t seed_mode = YK_SEED_COUNTER;    // YK_SEED_RANDOM_DEVICE: the runtime build's seeding
+  uint64_t seed_key = 0;                   // RANDOM_DEVICE key (0: a fresh one per call)
+  double t_min = 0.001;                    // raytracer.hpp:27
+};
+
 // One device context: the render loop of source.cpp:122-172 on the GPU.
 class renderer {
  public:
@@ -164,6 +172,13 @@ class renderer {
   // image_t bytes of the whole image: W*H*3, row 0 at the top (source.cpp:70-71,224-226)
   std::vector<uint8_t> render(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
                               uint32_t seed0, double t_min = 0.001) {
+    render_options o;
+    o.t_min = t_min;
+    return render(width, height, spp, max_depth, seed0, o);
+  }
+
+  std::vector<uint8_t> render(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
+                              uint32_t seed0, const render_options& o) {
     yk_render_params p;
     std::memset(&p, 0, sizeof p);
     p.image_width = width;
@@ -174,9 +189,11 @@ class renderer {
     p.row_begin = 0;
     p.row_count = height;
     p.row_stride = 1;
-    p.precision = YK_PRECISION_FP64;
+    p.precision = o.precision;
     p.rng = YK_RNG_MT19937;
-    p.t_min = t_min;
+    p.seed_mode = o.seed_mode;
+    p.seed_key = o.seed_key;
+    p.t_min = o.t_min;
     std::vector<uint8_t> img((size_t)width * height * 3);
     check(ykgpu_render(ctx_, &p, img.data()), "ykgpu_render");
     return img;

@@ -35,20 +35,38 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 2u
+#define YKGPU_ABI_VERSION 3u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 and DIELECTRIC are extensions needed by BASELINE configs 2-5 (no
  * reference oracle exists for them: parity unpinned). */
 enum { YK_MATERIAL_LAMBERTIAN = 0, YK_MATERIAL_METAL = 1, YK_MATERIAL_DIELECTRIC = 2 };
 
-/* Arithmetic of the per-sample path.  FP64 reproduces the reference (T = double,
- * source.cpp:98) bit for bit. */
-enum { YK_PRECISION_FP64 = 0 };
+/* Arithmetic of the per-sample path (the T of yk::render<T>, source.cpp:98-99).
+ * FP64 is render() as shipped (T = double), bit for bit.  FP32 is the same template with
+ * T = float: geometry, camera, canonicals (generate_canonical<float> takes ONE 32-bit draw,
+ * random.hpp:161-183) and math::sqrt in float; colours, attenuation and the per-pixel sum stay
+ * double (raytracer<T, double>, lambertian<double>, source.cpp:100-111).  Sphere centres, radii
+ * and camera vectors are the records' doubles rounded to float.  (As shipped, render<float>
+ * does not compile — sphere's deduction guide rejects the double radius literals — so FP32 is
+ * pinned against the reference's headers with the literals written as T(...): DESIGN.md §2.)
+ * FP32 uses the linear closest-hit scan (the BVH culling proof of DESIGN.md §4 is for FP64). */
+enum { YK_PRECISION_FP64 = 0, YK_PRECISION_FP32 = 1 };
 
 /* Random stream.  MT19937 = yk::mt19937 (random.hpp:148-151) seeded per sample with
  * seed0 + (y*W + x)*spp + s in uint32 arithmetic (source.cpp:154-158). */
 enum { YK_RNG_MT19937 = 0 };
+
+/* Per-sample seed of the mt19937 (yk_render_params.seed_mode).
+ * COUNTER: seed0 + (y*W + x)*spp + s in uint32 arithmetic — the constexpr build
+ *   (source.cpp:118-120,154-158); reproducible, the parity mode.
+ * RANDOM_DEVICE: the runtime build seeds every sample from std::random_device (source.cpp:159).
+ *   Here one 64-bit key per call (params.seed_key; 0 = draw it from std::random_device on the
+ *   host, reported in yk_render_stats.seed_key) is hashed with the sample's linear index
+ *   ((y*W + x)*spp + s, 64-bit): z = key + (idx+1)*0x9E3779B97F4A7C15, splitmix64 finaliser,
+ *   seed = high 32 bits.  Independent seeds per sample like the reference's runtime build;
+ *   reproducible when the key is given. */
+enum { YK_SEED_COUNTER = 0, YK_SEED_RANDOM_DEVICE = 1 };
 
 /* yk_render_params.flags */
 enum {
@@ -101,8 +119,9 @@ typedef struct yk_render_params {
   uint32_t precision;         /* YK_PRECISION_*                                         */
   uint32_t rng;               /* YK_RNG_*                                               */
   uint32_t flags;             /* YK_FLAG_*                                              */
-  uint32_t reserved;
+  uint32_t seed_mode;         /* YK_SEED_*                                              */
   double t_min;               /* 0.001 in the reference (raytracer.hpp:27)              */
+  uint64_t seed_key;          /* YK_SEED_RANDOM_DEVICE only (0: draw one per call)      */
 } yk_render_params;
 
 typedef struct yk_render_stats {
@@ -128,6 +147,7 @@ typedef struct yk_render_stats {
                               the first refill that found no pixel left, of the last wave
                               exit (last launch of the call)                              */
   uint64_t diag[4];        /* diagnostic builds only: [0] leaf tests with disc >= 0       */
+  uint64_t seed_key;       /* the key a YK_SEED_RANDOM_DEVICE render used (0 otherwise) */
   uint32_t launches;       /* path-tracing launches in the call                        */
   uint32_t grid_blocks;    /* persistent grid size                                     */
 } yk_render_stats;
@@ -163,6 +183,10 @@ int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* params, double
  * to_color3b in the render uses -- on n host doubles (in and out may alias).  The tests check it
  * against the reference's loop. */
 int ykgpu_math_sqrt(ykgpu_context* ctx, const double* in, double* out, uint64_t n);
+
+/* Same for the FP32 path's math::sqrt<float> (loop in float, s / 2.0 and the halving in
+ * double then rounded, exactly as math.hpp:10-19 reads for T = float) on n host floats. */
+int ykgpu_math_sqrt_f32(ykgpu_context* ctx, const float* in, float* out, uint64_t n);
 
 /* Diagnostics: the renderer's vector / scalar division (the normalisations and normals of
  * sphere.hpp / vec3.hpp) on n host triples: out3[3i+k] = num3[3i+k] / den[i].  It must equal

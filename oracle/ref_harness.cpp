@@ -24,6 +24,7 @@
 //   ref_harness render  <scene> W H spp depth seed0 out.rgb [out.sums]
 //   ref_harness samples <scene> W H spp depth seed0 y x s [y x s ...]   (per-sample colours, hex)
 //   ref_harness kat                                                   (RNG / sqrt / canonical KATs)
+//   render32 / samples32: the same with T = float (render<float>(); radius literals as T(...))
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -51,7 +52,8 @@
 
 namespace {
 
-using P = yk::pos3<double, yk::world_tag>;
+template <class T>
+using P = yk::pos3<T, yk::world_tag>;
 using L = yk::lambertian<double>;
 using M = yk::metal<double>;
 
@@ -65,56 +67,63 @@ struct counting_gen {
   result_type operator()() { ++n; return (*g)(); }
 };
 
+template <class T>
 auto scene_ref4() {
-  return yk::hittable_list<double>{}
-      .add(yk::sphere(P(0, 0, -1), 0.5, L({0.7, 0.3, 0.3})))
-      .add(yk::sphere(P(0, -100.5, -1), 100.0, L({0.8, 0.8, 0.0})))
-      .add(yk::sphere(P(-1.0, 0.0, -1.0), 0.5, M({0.8, 0.8, 0.8})))
-      .add(yk::sphere(P(1.0, 0.0, -1.0), 0.5, M({0.8, 0.6, 0.2})));
+  return yk::hittable_list<T>{}
+      .add(yk::sphere(P<T>(0, 0, -1), T(0.5), L({0.7, 0.3, 0.3})))
+      .add(yk::sphere(P<T>(0, -100.5, -1), T(100.0), L({0.8, 0.8, 0.0})))
+      .add(yk::sphere(P<T>(-1.0, 0.0, -1.0), T(0.5), M({0.8, 0.8, 0.8})))
+      .add(yk::sphere(P<T>(1.0, 0.0, -1.0), T(0.5), M({0.8, 0.6, 0.2})));
 }
 
+template <class T>
 auto scene_lambert3() {
-  return yk::hittable_list<double>{}
-      .add(yk::sphere(P(0, 0, -1), 0.5, L({0.7, 0.3, 0.3})))
-      .add(yk::sphere(P(0, -100.5, -1), 100.0, L({0.8, 0.8, 0.0})))
-      .add(yk::sphere(P(-1.0, 0.0, -1.0), 0.5, L({0.8, 0.8, 0.8})));
+  return yk::hittable_list<T>{}
+      .add(yk::sphere(P<T>(0, 0, -1), T(0.5), L({0.7, 0.3, 0.3})))
+      .add(yk::sphere(P<T>(0, -100.5, -1), T(100.0), L({0.8, 0.8, 0.0})))
+      .add(yk::sphere(P<T>(-1.0, 0.0, -1.0), T(0.5), L({0.8, 0.8, 0.8})));
 }
 
+template <class T>
 auto scene_mixed12() {
-  return yk::hittable_list<double>{}
-      .add(yk::sphere(P(0, -100.5, -1), 100.0, L({0.8, 0.8, 0.0})))
-      .add(yk::sphere(P(0, 0, -1), 0.5, L({0.1, 0.2, 0.5})))
-      .add(yk::sphere(P(-1.0, 0.0, -1.0), 0.5, M({0.8, 0.8, 0.8})))
-      .add(yk::sphere(P(1.0, 0.0, -1.0), 0.5, M({0.8, 0.6, 0.2})))
-      .add(yk::sphere(P(0, 0, -1), 0.5, M({0.9, 0.9, 0.9})))
-      .add(yk::sphere(P(-0.5, 0.6, -1.5), 0.3, L({0.9, 0.1, 0.1})))
-      .add(yk::sphere(P(0.5, 0.6, -1.5), 0.3, M({0.2, 0.9, 0.2})))
-      .add(yk::sphere(P(0, -0.3, -0.6), 0.15, L({0.2, 0.2, 0.9})))
-      .add(yk::sphere(P(0.3, 0.1, -0.45), 0.1, M({0.95, 0.95, 0.95})))
-      .add(yk::sphere(P(-0.35, -0.35, -0.7), 0.12, L({0.5, 0.9, 0.5})))
-      .add(yk::sphere(P(0, 1.2, -2.5), 0.6, L({0.7, 0.7, 0.7})))
-      .add(yk::sphere(P(1.0, 0.0, -1.0), 0.25, L({0.3, 0.3, 0.3})));
+  return yk::hittable_list<T>{}
+      .add(yk::sphere(P<T>(0, -100.5, -1), T(100.0), L({0.8, 0.8, 0.0})))
+      .add(yk::sphere(P<T>(0, 0, -1), T(0.5), L({0.1, 0.2, 0.5})))
+      .add(yk::sphere(P<T>(-1.0, 0.0, -1.0), T(0.5), M({0.8, 0.8, 0.8})))
+      .add(yk::sphere(P<T>(1.0, 0.0, -1.0), T(0.5), M({0.8, 0.6, 0.2})))
+      .add(yk::sphere(P<T>(0, 0, -1), T(0.5), M({0.9, 0.9, 0.9})))
+      .add(yk::sphere(P<T>(-0.5, 0.6, -1.5), T(0.3), L({0.9, 0.1, 0.1})))
+      .add(yk::sphere(P<T>(0.5, 0.6, -1.5), T(0.3), M({0.2, 0.9, 0.2})))
+      .add(yk::sphere(P<T>(0, -0.3, -0.6), T(0.15), L({0.2, 0.2, 0.9})))
+      .add(yk::sphere(P<T>(0.3, 0.1, -0.45), T(0.1), M({0.95, 0.95, 0.95})))
+      .add(yk::sphere(P<T>(-0.35, -0.35, -0.7), T(0.12), L({0.5, 0.9, 0.5})))
+      .add(yk::sphere(P<T>(0, 1.2, -2.5), T(0.6), L({0.7, 0.7, 0.7})))
+      .add(yk::sphere(P<T>(1.0, 0.0, -1.0), T(0.25), L({0.3, 0.3, 0.3})));
 }
 
 // two huge facing lambertian walls: long bounce chains (draws > 227 and > 624 at depth 200)
+template <class T>
 auto scene_walls2() {
-  return yk::hittable_list<double>{}
-      .add(yk::sphere(P(0, -300.5, -1), 300.0, L({0.9, 0.85, 0.8})))
-      .add(yk::sphere(P(0, 300.5, -1), 300.0, L({0.8, 0.9, 0.95})));
+  return yk::hittable_list<T>{}
+      .add(yk::sphere(P<T>(0, -300.5, -1), T(300.0), L({0.9, 0.85, 0.8})))
+      .add(yk::sphere(P<T>(0, 300.5, -1), T(300.0), L({0.8, 0.9, 0.95})));
 }
 
 struct job {
   std::uint32_t W, H, spp, depth, seed0;
 };
 
-template <class World>
+// T = double is render() as shipped (source.cpp:98); T = float is render<float>(): geometry,
+// camera, canonicals (one draw each) and math::sqrt in float, colour still double
+// (raytracer<T, double>, lambertian<double>).
+template <class T, class World>
 yk::color3d sample_color(const World& world, const job& j, std::uint32_t y, std::uint32_t x,
                          std::uint32_t s, std::uint64_t* draws) {
-  const yk::raytracer<double, double> tracer = {};
-  const yk::camera<double> cam = {};
+  const yk::raytracer<T, double> tracer = {};
+  const yk::camera<T> cam = {};
   yk::mt19937 g(j.seed0 + (y * j.W + x) * j.spp + s);
   counting_gen gen{&g};
-  yk::uniform_real_distribution<double> dist(0, 1);
+  yk::uniform_real_distribution<T> dist(0, 1);
   auto u = (x + dist(gen)) / j.W;
   auto v = (j.H - y - 1 + dist(gen)) / j.H;
   auto c = tracer.ray_color(cam.get_ray(u, v), world, j.depth, gen);
@@ -122,7 +131,7 @@ yk::color3d sample_color(const World& world, const job& j, std::uint32_t y, std:
   return c;
 }
 
-template <class World>
+template <class T, class World>
 int render(const World& world, const job& j, const char* out_rgb, const char* out_sums) {
   std::vector<unsigned char> rgb(std::size_t(j.W) * j.H * 3);
   std::vector<double> sums(std::size_t(j.W) * j.H * 3);
@@ -131,7 +140,7 @@ int render(const World& world, const job& j, const char* out_rgb, const char* ou
       auto iota = std::views::iota(0u, j.spp);
       yk::color3d pc = std::transform_reduce(
           iota.begin(), iota.end(), yk::color3d(0, 0, 0), std::plus{},
-          [&](auto s) { return sample_color(world, j, y, x, s, nullptr); });
+          [&](auto s) { return sample_color<T>(world, j, y, x, s, nullptr); });
       const std::size_t i = std::size_t(y) * j.W + x;
       sums[3 * i + 0] = pc.r;
       sums[3 * i + 1] = pc.g;
@@ -158,7 +167,7 @@ int render(const World& world, const job& j, const char* out_rgb, const char* ou
   return 0;
 }
 
-template <class World>
+template <class T, class World>
 int samples(const World& world, const job& j, int argc, char** argv) {
   std::printf("[\n");
   for (int k = 0; k + 2 < argc; k += 3) {
@@ -166,7 +175,7 @@ int samples(const World& world, const job& j, int argc, char** argv) {
     std::uint32_t x = std::strtoul(argv[k + 1], nullptr, 10);
     std::uint32_t s = std::strtoul(argv[k + 2], nullptr, 10);
     std::uint64_t n = 0;
-    auto c = sample_color(world, j, y, x, s, &n);
+    auto c = sample_color<T>(world, j, y, x, s, &n);
     std::printf("  {\"y\": %u, \"x\": %u, \"s\": %u, \"draws\": %llu, \"rgb\": [\"%a\", \"%a\", \"%a\"]}%s\n",
                 y, x, s, (unsigned long long)n, c.r, c.g, c.b, (k + 5 < argc) ? "," : "");
   }
@@ -195,7 +204,32 @@ int kat() {
     }
     std::printf("]%s\n", (k + 1 < sizeof(seeds) / sizeof(seeds[0])) ? "," : "");
   }
-  std::printf("  },\n  \"newton_sqrt\": [");
+  std::printf("  },\n  \"canonical01_f32\": {\n");
+  for (std::size_t k = 0; k < sizeof(seeds) / sizeof(seeds[0]); ++k) {
+    yk::mt19937 g(seeds[k]);
+    yk::uniform_real_distribution<float> d01(0, 1), dpm(-1, 1);
+    std::printf("    \"%u\": [", seeds[k]);
+    for (int i = 0; i < 64; ++i) {
+      float v = (i % 3 == 2) ? dpm(g) : d01(g);
+      std::printf("%s\"%a\"", i ? ", " : "", (double)v);
+    }
+    std::printf("]%s\n", (k + 1 < sizeof(seeds) / sizeof(seeds[0])) ? "," : "");
+  }
+  std::printf("  },\n  \"newton_sqrt_f32\": [");
+  {
+    std::vector<float> fs = {0.0f, 1.0f, 2.0f, 4.0f, 0.25f, 1e-30f, 1e-45f, 1e30f, 3.0f, 0.999f, 1e-8f,
+                             3.4e38f, 1.2e-38f};
+    std::uint64_t sf = 0x2545F4914F6CDD1Dull;
+    for (int i = 0; i < 500; ++i) {
+      sf = sf * 6364136223846793005ull + 1442695040888963407ull;
+      float m = 1.0f + float(sf >> 41) * 0x1p-23f;
+      int e = int((sf >> 3) % 60) - 30;
+      fs.push_back(std::ldexp(m, e));
+    }
+    for (std::size_t i = 0; i < fs.size(); ++i)
+      std::printf("%s[\"%a\", \"%a\"]", i ? ", " : "", (double)fs[i], (double)yk::math::sqrt(fs[i]));
+  }
+  std::printf("],\n  \"newton_sqrt\": [");
   // deterministic spread of inputs (LCG-scrambled mantissas over many binades) plus edges
   std::vector<double> xs = {0.0, 1.0, 2.0, 4.0, 0.25, 1e-300, 5e-324, 1e300, 3.0, 0.999, 1e-8};
   std::uint64_t st = 0x9E3779B97F4A7C15ull;
@@ -211,10 +245,20 @@ int kat() {
   return 0;
 }
 
-template <class World>
+template <class T, class World>
 int dispatch_world(const World& w, const char* mode, const job& j, int argc, char** argv) {
-  if (!std::strcmp(mode, "render")) return render(w, j, argv[0], argc > 1 ? argv[1] : nullptr);
-  return samples(w, j, argc, argv);
+  if (!std::strncmp(mode, "render", 6)) return render<T>(w, j, argv[0], argc > 1 ? argv[1] : nullptr);
+  return samples<T>(w, j, argc, argv);
+}
+
+template <class T>
+int dispatch(const std::string& scene, const char* mode, const job& j, int argc, char** argv) {
+  if (scene == "ref4") return dispatch_world<T>(scene_ref4<T>(), mode, j, argc, argv);
+  if (scene == "lambert3") return dispatch_world<T>(scene_lambert3<T>(), mode, j, argc, argv);
+  if (scene == "mixed12") return dispatch_world<T>(scene_mixed12<T>(), mode, j, argc, argv);
+  if (scene == "walls2") return dispatch_world<T>(scene_walls2<T>(), mode, j, argc, argv);
+  std::fprintf(stderr, "unknown scene %s\n", scene.c_str());
+  return 2;
 }
 
 }  // namespace
@@ -229,10 +273,8 @@ int main(int argc, char** argv) {
         (std::uint32_t)std::strtoul(argv[5], nullptr, 10), (std::uint32_t)std::strtoul(argv[6], nullptr, 10),
         (std::uint32_t)std::strtoul(argv[7], nullptr, 10)};
   const std::string scene = argv[2];
-  if (scene == "ref4") return dispatch_world(scene_ref4(), argv[1], j, argc - 8, argv + 8);
-  if (scene == "lambert3") return dispatch_world(scene_lambert3(), argv[1], j, argc - 8, argv + 8);
-  if (scene == "mixed12") return dispatch_world(scene_mixed12(), argv[1], j, argc - 8, argv + 8);
-  if (scene == "walls2") return dispatch_world(scene_walls2(), argv[1], j, argc - 8, argv + 8);
-  std::fprintf(stderr, "unknown scene %s\n", scene.c_str());
-  return 2;
+  // render32 / samples32: the same loop instantiated with T = float
+  const bool f32 = std::strstr(argv[1], "32") != nullptr;
+  return f32 ? dispatch<float>(scene, argv[1], j, argc - 8, argv + 8)
+             : dispatch<double>(scene, argv[1], j, argc - 8, argv + 8);
 }

@@ -74,61 +74,6 @@ static uint32_t mt_next(mt_t* g) {
   return z;
 }
 
-/* generate_canonical<double, 53>: random.hpp:161-183.  r = 2^32, so m = 2 draws:
- * sum = u0*1 + u1*2^32 (one rounding in the second add), ret = sum / 2^64, clamped below 1. */
-static double mt_canonical(mt_t* g) {
-  double sum = 0.0, tmp = 1.0;
-  sum += (double)mt_next(g) * tmp;
-  tmp *= 4294967296.0;
-  sum += (double)mt_next(g) * tmp;
-  tmp *= 4294967296.0;
-  double ret = sum / tmp;
-  if (ret >= 1.0) ret = 1.0 - 0x1p-53; /* 1 - epsilon/2 */
-  return ret;
-}
-
-/* uniform_real_distribution<double>::operator(): random.hpp:273-278: c*(b-a)+a */
-static double mt_uniform(mt_t* g, double a, double b) { return (mt_canonical(g) * (b - a)) + a; }
-
-/* ------------------------------------------------------------------ math.hpp:10-19 */
-static double nsqrt(double s) {
-  double x = s / 2.0, prev = 0.0;
-  int guard = 0; /* never reached for finite s; keeps a NaN input from spinning forever */
-  while (x != prev && guard++ < 4096) {
-    prev = x;
-    x = (x + s / x) / 2.0;
-  }
-  return x;
-}
-
-/* ------------------------------------------------------------------ vec3 helpers (vec3.hpp) */
-typedef struct { double x, y, z; } v3;
-static inline v3 v3_add(v3 a, v3 b) { v3 r = {a.x + b.x, a.y + b.y, a.z + b.z}; return r; }
-static inline v3 v3_sub(v3 a, v3 b) { v3 r = {a.x - b.x, a.y - b.y, a.z - b.z}; return r; }
-static inline v3 v3_mul(v3 a, double s) { v3 r = {a.x * s, a.y * s, a.z * s}; return r; }
-static inline v3 v3_div(v3 a, double s) { v3 r = {a.x / s, a.y / s, a.z / s}; return r; }
-static inline v3 v3_neg(v3 a) { v3 r = {-a.x, -a.y, -a.z}; return r; }
-static inline double v3_dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; } /* :145-147 */
-static inline double v3_len2(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }      /* :129 */
-static inline v3 v3_normalized(v3 a) { return v3_div(a, nsqrt(v3_len2(a))); }        /* :127,132 */
-/* near_zero, vec3.hpp:76-80 — note the reference tests x twice and never z */
-static inline int v3_near_zero(v3 a) {
-  double ax = a.x > 0 ? a.x : -a.x, ay = a.y > 0 ? a.y : -a.y;
-  return (ax < 1e-8) && (ay < 1e-8) && (ax < 1e-8);
-}
-/* reflect, vec3.hpp:199-202: v - 2*dot(v,n)*n */
-static inline v3 v3_reflect(v3 v, v3 n) { return v3_sub(v, v3_mul(n, 2 * v3_dot(v, n))); }
-static inline v3 v3_of(const double* p) { v3 r = {p[0], p[1], p[2]}; return r; }
-
-/* vec3::random(gen, -1, 1): vec3.hpp:134-142, x then y then z */
-static inline v3 v3_random(mt_t* g, double lo, double hi) {
-  v3 r;
-  r.x = mt_uniform(g, lo, hi);
-  r.y = mt_uniform(g, lo, hi);
-  r.z = mt_uniform(g, lo, hi);
-  return r;
-}
-
 typedef struct { double r, g, b; } c3;
 
 /* ------------------------------------------------------------------ scene */
@@ -141,131 +86,29 @@ typedef struct {
   int as_shipped; /* seed every sample from /dev/urandom like the runtime build (timing only) */
 } world_t;
 
-typedef struct {
-  v3 p, normal;
-  double t;
-  uint32_t id;
-  int front_face;
-} hit_t;
+/* ------------------------------------------------------------------ the path, per real type */
+static const double kEps_d = 0x1p-52; /* numeric_limits<double>::epsilon() */
+static const float kEps_f = 0x1p-23f; /* numeric_limits<float>::epsilon()  */
 
-/* sphere::hit_impl, sphere.hpp:25-48; set_face_normal, hittable.hpp:23-27 */
-static int sphere_hit(const yk_sphere* sp, v3 o, v3 d, double t_min, double t_max, hit_t* rec) {
-  v3 c = v3_of(sp->center);
-  v3 oc = v3_sub(o, c);
-  double a = v3_len2(d);
-  double half_b = v3_dot(oc, d);
-  double cc = v3_len2(oc) - sp->radius * sp->radius;
-  double disc = half_b * half_b - a * cc;
-  if (disc < 0) return 0;
-  double sq = nsqrt(disc);
-  double root = (-half_b - sq) / a;
-  if (root < t_min || t_max < root) {
-    root = (-half_b + sq) / a;
-    if (root < t_min || t_max < root) return 0;
-  }
-  rec->t = root;
-  rec->p = v3_add(o, v3_mul(d, root)); /* ray::at, ray.hpp:16-19 */
-  v3 outward = v3_div(v3_sub(rec->p, c), sp->radius);
-  rec->front_face = v3_dot(d, outward) < 0;
-  rec->normal = rec->front_face ? outward : v3_neg(outward);
-  return 1;
-}
+#define R double
+#define SFX(name) name##_d
+#define YKO_CANON_DRAWS 2
+#include "yk_oracle_path.h"
+#undef R
+#undef SFX
+#undef YKO_CANON_DRAWS
 
-/* hittable_list::hit_impl, hittable_list.hpp:32-58: ordered scan, shrinking closest_so_far,
- * the last accepted object (= closest, ties to the later index) wins. */
-static int world_hit(world_t* w, v3 o, v3 d, double t_min, double t_max, hit_t* out) {
-  double closest = t_max;
-  int any = 0;
-  hit_t tmp;
-  for (uint32_t i = 0; i < w->n; ++i) {
-    w->tests++;
-    if (sphere_hit(&w->s[i], o, d, t_min, closest, &tmp)) {
-      closest = tmp.t;
-      tmp.id = i;
-      *out = tmp;
-      any = 1;
-    }
-  }
-  return any;
-}
+#define R float
+#define SFX(name) name##_f
+#define YKO_CANON_DRAWS 1
+#include "yk_oracle_path.h"
+#undef R
+#undef SFX
+#undef YKO_CANON_DRAWS
 
-/* Schlick, RTIOW (extension) — (1-c)^5 as an explicit left-to-right product */
-static double reflectance(double cosine, double ref_idx) {
-  double r0 = (1 - ref_idx) / (1 + ref_idx);
-  r0 = r0 * r0;
-  double x = 1 - cosine;
-  return r0 + (1 - r0) * ((((x * x) * x) * x) * x);
-}
-
-/* scatter dispatch hittable_list.hpp:60-73 → sphere.hpp:50-54 → material.hpp */
-static int scatter(const yk_sphere* sp, v3 rd, const hit_t* rec, mt_t* g, c3* att, v3* dir) {
-  switch (sp->material) {
-    case YK_MATERIAL_LAMBERTIAN: { /* material.hpp:50-59, random_unit_vector :33-36 */
-      v3 ru = v3_random(g, -1, 1);
-      ru = v3_div(ru, nsqrt(v3_len2(ru))); /* normalize(): *this /= length() */
-      v3 sd = v3_add(rec->normal, ru);
-      if (v3_near_zero(sd)) sd = rec->normal;
-      *dir = sd;
-      att->r = sp->albedo[0]; att->g = sp->albedo[1]; att->b = sp->albedo[2];
-      return 1;
-    }
-    case YK_MATERIAL_METAL: { /* material.hpp:67-75 (+ fuzz extension) */
-      v3 refl = v3_reflect(v3_normalized(rd), rec->normal);
-      if (sp->fuzz > 0) { /* extension: random_in_unit_sphere, material.hpp:27-30 */
-        v3 ru = v3_random(g, -1, 1);
-        ru = v3_div(ru, nsqrt(v3_len2(ru)));
-        double k = mt_uniform(g, 0.01, 0.99);
-        refl = v3_add(refl, v3_mul(v3_mul(ru, k), sp->fuzz));
-      }
-      if (v3_dot(refl, rec->normal) > 0) {
-        *dir = refl;
-        att->r = sp->albedo[0]; att->g = sp->albedo[1]; att->b = sp->albedo[2];
-        return 1;
-      }
-      return 0;
-    }
-    case YK_MATERIAL_DIELECTRIC: { /* extension (RTIOW dielectric, yk-style arithmetic) */
-      double ratio = rec->front_face ? (1.0 / sp->ior) : sp->ior;
-      v3 unit = v3_normalized(rd);
-      double ct = v3_dot(v3_neg(unit), rec->normal);
-      if (!(ct < 1.0)) ct = 1.0;
-      double st = nsqrt(1.0 - ct * ct);
-      int cannot = ratio * st > 1.0;
-      if (cannot || reflectance(ct, ratio) > mt_uniform(g, 0, 1)) {
-        *dir = v3_reflect(unit, rec->normal);
-      } else {
-        v3 perp = v3_mul(v3_add(unit, v3_mul(rec->normal, ct)), ratio);
-        double pl = 1.0 - v3_len2(perp);
-        v3 par = v3_mul(rec->normal, -nsqrt(pl < 0 ? -pl : pl));
-        *dir = v3_add(perp, par);
-      }
-      att->r = 1.0; att->g = 1.0; att->b = 1.0;
-      return 1;
-    }
-  }
-  return 0;
-}
-
-/* raytracer::ray_color, raytracer.hpp:19-37 — kept recursive, exactly like the reference */
-static c3 ray_color(world_t* w, v3 o, v3 d, uint32_t depth, mt_t* g, uint64_t* segs) {
-  c3 black = {0, 0, 0};
-  if (depth == 0) return black;
-  hit_t rec;
-  if (segs) (*segs)++;
-  if (world_hit(w, o, d, w->p->t_min, INFINITY, &rec)) {
-    c3 att;
-    v3 nd;
-    if (scatter(&w->s[rec.id], d, &rec, g, &att, &nd)) {
-      c3 in = ray_color(w, rec.p, nd, depth - 1, g, segs);
-      c3 r = {att.r * in.r, att.g * in.g, att.b * in.b};
-      return r;
-    }
-    return black;
-  }
-  double t = (v3_normalized(d).y + 1.0) / 2;
-  c3 r = {(1.0 - t) * 1.0 + t * 0.5, (1.0 - t) * 1.0 + t * 0.7, (1.0 - t) * 1.0 + t * 1.0};
-  return r;
-}
+/* the double names the rest of this file (and its KAT exports) use */
+#define mt_uniform uniform_d
+#define nsqrt nsqrt_d
 
 /* The runtime build's seed, source.cpp:159: a std::random_device constructed per sample.
  * libstdc++'s random_device opens its entropy source, reads one word and closes it again; this
@@ -281,34 +124,29 @@ static uint32_t random_device_u32(void) {
   return v;
 }
 
-/* One sample: source.cpp:154-166 (seed :154-158, jitter :160-164, get_ray camera.hpp:29-32
- * or the thin-lens extension). */
+/* YK_SEED_RANDOM_DEVICE: the runtime build gives every sample its own std::random_device seed
+ * (source.cpp:159).  The GPU cannot read an entropy device per sample, so the mode hashes one
+ * 64-bit key per call with the sample's linear index (splitmix64 finaliser, high word): seeds
+ * independent across samples, reproducible given the key (include/ykgpu.h). */
+static uint32_t seed_from_key(uint64_t key, uint64_t idx) {
+  uint64_t z = key + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+/* One sample: source.cpp:154-166 (seed :154-158, then trace_sample in the call's precision). */
 static c3 sample(world_t* w, uint32_t y, uint32_t x, uint32_t s, uint64_t* draws, uint64_t* segs) {
   const yk_render_params* p = w->p;
-  const yk_camera* cam = w->cam;
   mt_t g;
   uint32_t seed = p->seed0 + (y * p->image_width + x) * p->samples_per_pixel + s;
+  if (p->seed_mode == YK_SEED_RANDOM_DEVICE)
+    seed = seed_from_key(p->seed_key, ((uint64_t)y * p->image_width + x) * p->samples_per_pixel + s);
   if (w->as_shipped) seed = random_device_u32();
   mt_seed(&g, seed);
-  double u = (x + mt_uniform(&g, 0, 1)) / p->image_width;
-  double v = (p->image_height - y - 1 + mt_uniform(&g, 0, 1)) / p->image_height;
-  v3 org = v3_of(cam->origin);
-  v3 dir = v3_add(v3_add(v3_of(cam->lower_left_corner), v3_mul(v3_of(cam->horizontal), u)),
-                  v3_mul(v3_of(cam->vertical), v));
-  dir = v3_sub(dir, org);
-  if (cam->lens_radius > 0) { /* extension: random_in_unit_disk by rejection */
-    double px, py;
-    for (;;) {
-      px = mt_uniform(&g, -1, 1);
-      py = mt_uniform(&g, -1, 1);
-      if (px * px + py * py < 1.0) break;
-    }
-    double rx = px * cam->lens_radius, ry = py * cam->lens_radius;
-    v3 off = v3_add(v3_mul(v3_of(cam->lens_u), rx), v3_mul(v3_of(cam->lens_v), ry));
-    org = v3_add(org, off);
-    dir = v3_sub(dir, off);
-  }
-  c3 c = ray_color(w, org, dir, p->max_depth, &g, segs);
+  c3 c = p->precision == YK_PRECISION_FP32 ? trace_sample_f(w, &g, y, x, segs)
+                                           : trace_sample_d(w, &g, y, x, segs);
   if (draws) *draws = g.draws;
   return c;
 }
@@ -375,7 +213,9 @@ static int check(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_
   if (p->row_count && (p->row_stride == 0 ||
       (uint64_t)p->row_begin + (uint64_t)(p->row_count - 1) * p->row_stride >= p->image_height))
     return YK_ERR_INVALID;
-  if (p->precision != YK_PRECISION_FP64 || p->rng != YK_RNG_MT19937) return YK_ERR_UNSUPPORTED;
+  if ((p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32) || p->rng != YK_RNG_MT19937 ||
+      p->seed_mode > YK_SEED_RANDOM_DEVICE || (p->seed_mode == YK_SEED_RANDOM_DEVICE && !p->seed_key))
+    return YK_ERR_UNSUPPORTED;
   return YK_OK;
 }
 
@@ -457,3 +297,18 @@ double yko_newton_sqrt(double s) { return nsqrt(s); }
 void yko_newton_sqrt_n(const double* in, double* out, uint64_t n) {
   for (uint64_t i = 0; i < n; ++i) out[i] = nsqrt(in[i]);
 }
+
+/* FP32 path (render<float>): the KAT pattern with uniform_real_distribution<float> (one draw per
+ * canonical), and math::sqrt<float> over an array. */
+void yko_canonical_pattern_f32(uint32_t seed, uint32_t count, float* out) {
+  mt_t g;
+  mt_seed(&g, seed);
+  for (uint32_t i = 0; i < count; ++i) out[i] = (i % 3 == 2) ? uniform_f(&g, -1, 1) : uniform_f(&g, 0, 1);
+}
+
+void yko_newton_sqrt_f32_n(const float* in, float* out, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) out[i] = nsqrt_f(in[i]);
+}
+
+/* The per-sample seed of YK_SEED_RANDOM_DEVICE (include/ykgpu.h), for tests. */
+uint32_t yko_seed_from_key(uint64_t key, uint64_t idx) { return seed_from_key(key, idx); }

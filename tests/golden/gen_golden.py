@@ -48,6 +48,17 @@ CASES = [
     ("ref4", 48, 27, 4, 50, 4294967000, True),  # seed wraps mod 2^32 inside the image
     ("ref4", 33, 17, 5, 50, 7, True),           # odd, non-16:9 size, spp 5
 ]
+# render<float> (YK_PRECISION_FP32): the harness's render32 mode, same loop with T = float
+CASES_F32 = [
+    ("ref4", 16, 9, 2, 50, 404, True),
+    ("ref4", 200, 112, 8, 50, 404, False),      # config 1 shape
+    ("ref4", 200, 112, 64, 50, 404, False),
+    ("mixed12", 96, 54, 16, 50, 404, True),
+    ("walls2", 64, 36, 8, 200, 404, True),      # long paths (one draw per canonical in float)
+    ("ref4", 32, 18, 6, 50, 404, True),
+    ("ref4", 48, 27, 4, 50, 4294967000, True),
+    ("ref4", 33, 17, 5, 50, 7, True),
+]
 
 
 def sha(b: bytes) -> str:
@@ -94,8 +105,8 @@ def png_rgb(path):
     return bytes(out), W, H
 
 
-def case_name(scene, W, H, spp, depth, seed0):
-    return f"{scene}_{W}x{H}x{spp}_d{depth}_s{seed0}"
+def case_name(scene, W, H, spp, depth, seed0, f32=False):
+    return f"{scene}_{W}x{H}x{spp}_d{depth}_s{seed0}" + ("_f32" if f32 else "")
 
 
 def main():
@@ -112,16 +123,18 @@ def main():
     manifest["constexpr_build"] = {"file": "cx16_ref4.rgb", "scene": "ref4", "W": 16, "H": 9,
                                    "spp": 2, "depth": 50, "seed0": 404, "rgb_sha256": sha(rgb)}
 
-    # 2. harness renders
-    for scene, W, H, spp, depth, seed0, keep_sums in CASES:
-        name = case_name(scene, W, H, spp, depth, seed0)
+    # 2. harness renders (FP64 = render() as shipped, then FP32 = render<float>)
+    for f32, cases in ((False, CASES), (True, CASES_F32)):
+      for scene, W, H, spp, depth, seed0, keep_sums in cases:
+        name = case_name(scene, W, H, spp, depth, seed0, f32)
         with tempfile.TemporaryDirectory() as td:
             f_rgb, f_sums = os.path.join(td, "o.rgb"), os.path.join(td, "o.sums")
-            subprocess.run([HARNESS, "render", scene, str(W), str(H), str(spp), str(depth),
-                            str(seed0), f_rgb, f_sums], check=True)
+            subprocess.run([HARNESS, "render32" if f32 else "render", scene, str(W), str(H),
+                            str(spp), str(depth), str(seed0), f_rgb, f_sums], check=True)
             rgb, sums = open(f_rgb, "rb").read(), open(f_sums, "rb").read()
         entry = {"name": name, "scene": scene, "W": W, "H": H, "spp": spp, "depth": depth,
-                 "seed0": seed0, "rgb_file": name + ".rgb", "rgb_sha256": sha(rgb),
+                 "seed0": seed0, "precision": "fp32" if f32 else "fp64",
+                 "rgb_file": name + ".rgb", "rgb_sha256": sha(rgb),
                  "sums_sha256": sha(sums)}
         open(os.path.join(HERE, name + ".rgb"), "wb").write(rgb)
         if keep_sums:
@@ -137,10 +150,15 @@ def main():
     import oracle_lib
     import refscenes
     from uecraytracing_amd.records import make_params
-    for scene, W, H, spp, depth in [("ref4", 200, 112, 8, 50), ("mixed12", 96, 54, 16, 50),
-                                    ("walls2", 64, 36, 8, 200)]:
+    from uecraytracing_amd.records import PRECISION_FP32, PRECISION_FP64
+    for scene, W, H, spp, depth, f32 in [("ref4", 200, 112, 8, 50, False),
+                                         ("mixed12", 96, 54, 16, 50, False),
+                                         ("walls2", 64, 36, 8, 200, False),
+                                         ("ref4", 200, 112, 8, 50, True),
+                                         ("walls2", 64, 36, 8, 200, True)]:
         sph, cam = refscenes.SCENES[scene](), refscenes.reference_camera()
-        p = make_params(W, H, spp, depth, 404)
+        p = make_params(W, H, spp, depth, 404,
+                        precision=PRECISION_FP32 if f32 else PRECISION_FP64)
         cand = []
         for y in range(0, H, 3):
             for x in range(0, W, 5):
@@ -151,10 +169,12 @@ def main():
         pick = cand[:12] + cand[len(cand) // 2:len(cand) // 2 + 6] + cand[-4:]
         pick += [(0, 0, 0, 0), (0, H - 1, W - 1, spp - 1)]
         args = [str(v) for _, y, x, s in pick for v in (y, x, s)]
-        out = subprocess.run([HARNESS, "samples", scene, str(W), str(H), str(spp), str(depth),
-                              "404"] + args, check=True, capture_output=True, text=True).stdout
-        manifest["samples"][scene] = {"W": W, "H": H, "spp": spp, "depth": depth, "seed0": 404,
-                                      "points": json.loads(out)}
+        out = subprocess.run([HARNESS, "samples32" if f32 else "samples", scene, str(W), str(H),
+                              str(spp), str(depth), "404"] + args,
+                             check=True, capture_output=True, text=True).stdout
+        manifest["samples"][scene + ("_f32" if f32 else "")] = {
+            "W": W, "H": H, "spp": spp, "depth": depth, "seed0": 404,
+            "precision": "fp32" if f32 else "fp64", "points": json.loads(out)}
         print("samples", scene, "max draws", max(e["draws"] for e in json.loads(out)))
 
     # 4. KATs

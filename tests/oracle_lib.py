@@ -45,6 +45,12 @@ def load():
     lib.yko_newton_sqrt.restype = ctypes.c_double
     lib.yko_newton_sqrt_n.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     lib.yko_newton_sqrt_n.restype = None
+    lib.yko_canonical_pattern_f32.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    lib.yko_canonical_pattern_f32.restype = None
+    lib.yko_newton_sqrt_f32_n.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    lib.yko_newton_sqrt_f32_n.restype = None
+    lib.yko_seed_from_key.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+    lib.yko_seed_from_key.restype = ctypes.c_uint32
     _lib = lib
     return lib
 
@@ -117,3 +123,23 @@ def newton_sqrt_array(values):
     out = np.empty_like(a)
     load().yko_newton_sqrt_n(a.ctypes.data, out.ctypes.data, a.size)
     return out
+
+
+def canonical_pattern_f32(seed, count):
+    """The KAT pattern with uniform_real_distribution<float> (render<float>)."""
+    out = np.empty(count, np.float32)
+    load().yko_canonical_pattern_f32(seed, count, out.ctypes.data)
+    return out
+
+
+def newton_sqrt_f32(values):
+    """math::sqrt<float> (math.hpp:10-19 with T = float) over an array."""
+    a = np.ascontiguousarray(values, dtype=np.float32)
+    out = np.empty_like(a)
+    load().yko_newton_sqrt_f32_n(a.ctypes.data, out.ctypes.data, a.size)
+    return out
+
+
+def seed_from_key(key, idx):
+    """Per-sample seed of YK_SEED_RANDOM_DEVICE (include/ykgpu.h)."""
+    return load().yko_seed_from_key(key, idx)

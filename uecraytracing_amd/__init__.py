@@ -26,7 +26,7 @@ CLI_PATH = os.path.join(LIB_DIR, "raytrace")
 EXPORTS = (
     "ykgpu_abi_version", "ykgpu_last_error", "ykgpu_device_count", "ykgpu_context_create",
     "ykgpu_context_destroy", "ykgpu_set_scene", "ykgpu_render", "ykgpu_render_async",
-    "ykgpu_render_sums", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_div", "yk_camera_reference", "yk_camera_look",
+    "ykgpu_render_sums", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_sqrt_f32", "ykgpu_math_div", "yk_camera_reference", "yk_camera_look",
     "yk_scene_build", "yk_scene_write", "yk_scene_read", "yk_image_height_for",
 )
 SCENE_DIR = os.path.join(PKG_DIR, "scenes")  # committed scene files of the BASELINE configs
@@ -68,6 +68,7 @@ def load_library():
         "ykgpu_render_sums": ([c.c_void_p, P(RenderParams), c.c_void_p], c.c_int),
         "ykgpu_get_stats": ([c.c_void_p, P(RenderStats)], c.c_int),
         "ykgpu_math_sqrt": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
+        "ykgpu_math_sqrt_f32": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
         "ykgpu_math_div": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
         "yk_camera_reference": ([P(Camera)], c.c_int),
         "yk_camera_look": ([P(Camera), P(c.c_double), P(c.c_double), P(c.c_double), c.c_double,
@@ -81,7 +82,7 @@ def load_library():
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
         f.argtypes, f.restype = args, res
-    if lib.ykgpu_abi_version() != 2:
+    if lib.ykgpu_abi_version() != 3:
         raise YkError("ABI version mismatch")
     _lib = lib
     return lib
@@ -183,6 +184,13 @@ class Renderer:
         a = np.ascontiguousarray(values, dtype=np.float64)
         out = np.empty_like(a)
         _check(self._lib.ykgpu_math_sqrt(self._ctx, a.ctypes.data, out.ctypes.data, a.size))
+        return out
+
+    def math_sqrt_f32(self, values) -> np.ndarray:
+        """The FP32 path's math::sqrt<float> on a float32 array (diagnostic)."""
+        a = np.ascontiguousarray(values, dtype=np.float32)
+        out = np.empty_like(a)
+        _check(self._lib.ykgpu_math_sqrt_f32(self._ctx, a.ctypes.data, out.ctypes.data, a.size))
         return out
 
     def math_div(self, num3, den) -> np.ndarray:

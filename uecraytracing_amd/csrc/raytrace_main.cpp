@@ -11,9 +11,11 @@
 // reference scene (source.cpp:103-112), built with the same yk calls.
 //
 // Added (render parameters are compile-time macros in the reference): --width, --spp,
-// --depth, --scene, --scene-seed, --scene-file, --save-scene, --seed0, --device, --stats.  --seed0 fixes the per-sample seed
-// base (seed0 + (y*W+x)*spp + s, source.cpp:154-158); without it seed0 comes from
-// std::random_device, like the reference's runtime build draws every sample's seed from it.
+// --depth, --scene, --scene-seed, --scene-file, --save-scene, --seed0, --precision, --device,
+// --stats.  --seed0 fixes the per-sample seed base (seed0 + (y*W+x)*spp + s, the constexpr
+// build's formula, source.cpp:154-158); without it every sample gets its own seed from a
+// per-call std::random_device key (YK_SEED_RANDOM_DEVICE), like the reference's runtime build
+// (source.cpp:159).  --precision fp32 renders render<float> (T = float, source.cpp:98).
 // Verbose output: levels 1-2 print the reference's per-pixel / per-sample lines after the GPU
 // render, in the same order; level 3 (per-ray dumps, raytracer.hpp:21-25) is not available.
 #include <cmath>
@@ -64,6 +66,7 @@ const char* kHelp =
     "      --scene-file arg      load the scene from a yk-scene file (overrides --scene)\n"
     "      --save-scene arg      write the scene to a yk-scene file\n"
     "      --seed0 arg           per-sample seed base (default: random_device)\n"
+    "      --precision arg       fp64|fp32: the T of render<T> (default: fp64)\n"
     "      --device arg          GPU index (default: 0)\n"
     "      --stats               print kernel time and throughput\n";
 
@@ -76,6 +79,7 @@ struct args {
   int device = 0;
   bool have_seed0 = false;
   uint32_t seed0 = 0;
+  std::string precision = "fp64";
   std::string scene = "ref4";
   std::string scene_file, save_scene;
 };
@@ -127,6 +131,7 @@ args parse(int argc, char** argv) {
       else if (n == "scene-file") a.scene_file = value(i, n, inl);
       else if (n == "save-scene") a.save_scene = value(i, n, inl);
       else if (n == "seed0") { a.seed0 = to_u32(n, value(i, n, inl)); a.have_seed0 = true; }
+      else if (n == "precision") a.precision = value(i, n, inl);
       else throw option_error{"Option '" + n + "' does not exist"};
     } else if (s.size() > 1 && s[0] == '-') {
       for (size_t k = 1; k < s.size(); ++k) {
@@ -178,7 +183,15 @@ int main(int argc, char* argv[]) {
   if (!a.levels.empty()) verbose = a.levels.back();
 
   const uint32_t W = a.width, H = yk_image_height_for(W);
-  const uint32_t seed0 = a.have_seed0 ? a.seed0 : std::random_device{}();
+  const uint32_t seed0 = a.have_seed0 ? a.seed0 : 0u;
+  ykgpu::render_options ro;
+  ro.seed_mode = a.have_seed0 ? YK_SEED_COUNTER : YK_SEED_RANDOM_DEVICE;
+  if (a.precision == "fp32") {
+    ro.precision = YK_PRECISION_FP32;
+  } else if (a.precision != "fp64") {
+    std::cerr << "unknown precision " << a.precision << " (fp64|fp32)" << std::endl;
+    return EXIT_FAILURE;
+  }
   std::vector<uint8_t> image;
   try {
     ykgpu::renderer gpu(a.device);
@@ -223,7 +236,7 @@ int main(int argc, char* argv[]) {
       if (!a.save_scene.empty()) yk_scene_write(a.save_scene.c_str(), s.data(), n, &cam);
     }
     std::cout << "rendering..." << std::endl;
-    image = gpu.render(W, H, a.spp, a.depth, seed0);
+    image = gpu.render(W, H, a.spp, a.depth, seed0, ro);
     if (verbose) {
       for (uint32_t y = 0; y < H; ++y)
         for (uint32_t x = 0; x < W; ++x) {
@@ -240,7 +253,11 @@ int main(int argc, char* argv[]) {
     if (a.stats) {
       const yk_render_stats st = gpu.stats();
       std::cerr << "kernels " << st.kernel_ms << " ms, " << (double)st.samples / st.kernel_ms / 1e3
-                << " Msamples/s, seed0 " << seed0 << std::endl;
+                << " Msamples/s, ";
+      if (a.have_seed0)
+        std::cerr << "seed0 " << seed0 << std::endl;
+      else
+        std::cerr << "seed key 0x" << std::hex << st.seed_key << std::dec << std::endl;
     }
   } catch (const ykgpu::error& e) {
     std::cerr << e.what() << std::endl;

@@ -295,6 +295,24 @@ __device__ __forceinline__ uint32_t mt_next(MtLane& g) {
   return mt_temper(z);
 }
 
+// Per-sample seed (include/ykgpu.h YK_SEED_*).  COUNTER: seed0 + (y*W + x)*spp + s in uint32
+// arithmetic (source.cpp:154-158).  RANDOM_DEVICE: the call's 64-bit key hashed with the
+// sample's 64-bit linear index (splitmix64 finaliser, high word) — one independent seed per
+// sample, like the runtime build's std::random_device (source.cpp:159).
+__device__ __forceinline__ uint32_t sample_seed(uint32_t mode, uint64_t key, uint32_t seed0, uint32_t y,
+                                                uint32_t x, uint32_t W, uint32_t spp, uint32_t s) {
+#ifndef YK_SEED_COUNTER_ONLY  // (A/B timing builds: the random-device mode compiled out)
+  if (mode == 1u) {
+    uint64_t z = key + (((uint64_t)y * W + x) * spp + s + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 32);
+  }
+#endif
+  return seed0 + (y * W + x) * spp + s;
+}
+
 // generate_canonical<double,53> (random.hpp:161-183): two draws, sum = u0 + u1*2^32 rounded
 // once, divided by 2^64 (exact), clamped to 1 - eps/2.
 __device__ __forceinline__ double canonical(MtLane& g) {

@@ -1,0 +1,87 @@
+// yk_device_f32.hpp — per-lane arithmetic of one sample of render<float> (YK_PRECISION_FP32),
+// gfx950 device code.
+//
+// yk::render<T> with T = float (source.cpp:98-99): geometry, camera, canonicals and math::sqrt
+// in float; colours stay double (raytracer<T, double>, lambertian<double>), so the attenuation
+// products and the per-pixel sum are the FP64 path's.  Every expression keeps the reference's
+// C++ type promotions (a float meeting a double literal is promoted, e.g. near_zero's 1e-8 and
+// the sky's `y + 1.0`) and its association order; the file is compiled with -ffp-contract=off,
+// and float `/` and sqrtf are correctly rounded (hipcc's default
+// -fhip-fp32-correctly-rounded-divide-sqrt; the parity tests check the results bit for bit
+// against oracle/yk_oracle_path.h, which is pinned to the reference's own render<float>).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "yk_device.hpp"
+
+namespace ykf {
+
+struct v3 {
+  float x, y, z;
+};
+__device__ __forceinline__ v3 add(v3 a, v3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ v3 sub(v3 a, v3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ v3 mul(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ v3 divs(v3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ v3 neg(v3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  // vec3.hpp:145-147
+__device__ __forceinline__ float len2(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }      // vec3.hpp:129
+__device__ __forceinline__ v3 of(const double* p) { return {(float)p[0], (float)p[1], (float)p[2]}; }
+
+// math::sqrt<float> (math.hpp:10-19): `T x = s / 2.0` and `x = (x + s / x) / 2.0` halve in
+// double and round to float, which equals the float product by 0.5f (halving is exact, so both
+// are one rounding of the same value).  As for FP64 (yk_device.hpp), the loop's result is a
+// fixed point that does not depend on the start: for every positive float s in [2^-100, 2^100]
+// the loop started at the correctly rounded sqrtf(s) ends at the reference's value (checked
+// exhaustively over all 2^31 positive floats by tools/fsqrt_check.c: every float terminates,
+// at most 80 reference iterations, and only one input — outside that range — differs).
+__device__ __forceinline__ float nsqrt(float s, uint32_t& iters) {
+  float x = (s >= 0x1p-100f && s <= 0x1p100f) ? __builtin_sqrtf(s) : s * 0.5f;
+  float prev = 0.0f;
+  for (int guard = 0; x != prev && guard < 4096; ++guard) {  // the bound only matters for NaN/inf
+    prev = x;
+    x = (x + s / x) * 0.5f;
+    ++iters;
+  }
+  return x;
+}
+
+// reflect(): vec3.hpp:199-202, v - (2*dot(v,n))*n with `2 * dot` a float product
+__device__ __forceinline__ v3 reflect(v3 v, v3 n) { return sub(v, mul(n, 2.0f * dot(v, n))); }
+// near_zero(): vec3.hpp:76-80 — s = 1e-8 is a double, so |x| is compared after promotion; the
+// reference tests x twice and never z
+__device__ __forceinline__ bool near_zero(v3 a) {
+  const float ax = a.x > 0 ? a.x : -a.x, ay = a.y > 0 ? a.y : -a.y;
+  return ((double)ax < 1e-8) && ((double)ay < 1e-8) && ((double)ax < 1e-8);
+}
+
+// generate_canonical<float, 24> (random.hpp:161-183): m = max(1, (24 + 32) / 33) = 1 draw;
+// sum = float(u) (rounded to nearest), ret = sum / 2^32 (exact scaling), clamped to 1 - eps/2.
+__device__ __forceinline__ float canonical(ykd::MtLane& g) {
+  const float sum = (float)ykd::mt_next(g);
+  float r = sum * 0x1p-32f;
+  if (r >= 1.0f) r = 1.0f - 0x1p-24f;
+  return r;
+}
+// uniform_real_distribution<float>::operator() (random.hpp:273-278): c*(b-a)+a in float
+__device__ __forceinline__ float uniform(ykd::MtLane& g, float a, float b) { return (ykf::canonical(g) * (b - a)) + a; }
+// vec3<float>::random(gen, -1, 1) (vec3.hpp:134-142): x, then y, then z
+__device__ __forceinline__ v3 random_vec(ykd::MtLane& g, float lo, float hi) {
+  v3 r;
+  r.x = ykf::uniform(g, lo, hi);
+  r.y = ykf::uniform(g, lo, hi);
+  r.z = ykf::uniform(g, lo, hi);
+  return r;
+}
+
+// Schlick reflectance (dielectric extension; no reference code), in float
+__device__ __forceinline__ float reflectance(float cosine, float ref_idx) {
+  float r0 = (1.0f - ref_idx) / (1.0f + ref_idx);
+  r0 = r0 * r0;
+  const float x = 1.0f - cosine;
+  return r0 + (1.0f - r0) * ((((x * x) * x) * x) * x);
+}
+
+}  // namespace ykf

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <random>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -35,6 +36,7 @@
 #include "../../include/ykgpu.h"
 #include "yk_bvh.hpp"
 #include "yk_device.hpp"
+#include "yk_device_f32.hpp"
 
 using ykd::v3;
 
@@ -109,7 +111,8 @@ struct KernelArgs {
   uint32_t nspheres, pad_n, flags, id_stride;
   // A launch renders samples [s0, s0 + nsl / npix_slots) of every pixel: sample slot
   // i = s_local * npix_slots + p is sample s0 + s_local of tile pixel order[p].
-  uint32_t s0, nsl, npix_slots, pad_s;
+  uint32_t s0, nsl, npix_slots, seed_mode;  // seed_mode: YK_SEED_*
+  uint64_t seed_key;
   const uint32_t* __restrict__ order;  // p → tile pixel (kNoPixel: empty slot of an edge block)
   const uint32_t* __restrict__ warm;   // x_397 per sample slot of the launch
   double t_min;
@@ -123,6 +126,7 @@ struct KernelArgs {
   const uint32_t* __restrict__ leaf_ids;   // leaf slot → tuple index
   const SphereGeo* __restrict__ geo;
   const SphereMat* __restrict__ mat;
+  const float4* __restrict__ geo_f;  // FP32 path: (cx, cy, cz, r*r) rounded to float, tuple order
   double* col;                       // sample colours, SoA: col[c * nsl + i]
   uint32_t* pixel_counter;           // sample-slot counter
   uint32_t* mt_scratch;
@@ -224,7 +228,8 @@ constexpr uint32_t kNoPixel = 0xffffffffu;
 // Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread,
 // one 16-B store.  out[i] = x_397(seed(i)), i = (pix - pix_base) * spp + s.
 struct WarmArgs {
-  uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, pad;
+  uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode;
+  uint64_t seed_key;
   const uint32_t* order;
   uint64_t n;  // sample slots in the launch
   uint32_t* out;
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       const uint32_t sm = wa.s0 + sl;
       const uint32_t tr = pix / wa.W, xx = pix - tr * wa.W;
       const uint32_t y = wa.row_begin + tr * wa.row_stride;
-      x[k] = wa.seed0 + (y * wa.W + xx) * wa.spp + sm;
+      x[k] = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, sm);
     }
     ykd::mt_walk397x4(x);
     if (i0 + 4 <= wa.n) {
@@ -317,14 +322,50 @@ __global__ __launch_bounds__(256) void yk_math_sqrt(const double* in, double* ou
   if (i < n) out[i] = ykd::nsqrt(in[i]);
 }
 
+// Refill of the persistent kernels: lanes without a path take the next sample slots from the
+// wave's reserve, one atomic per kClaim slots.  Every lane runs it, so the reserve (res_base,
+// res_left) stays wave-uniform.  (A pixel is not a lane's unit of work: the samples of a pixel
+// are independent, only their SUM is ordered, and yk_reduce_samples does that.)  Returns true
+// when this lane has no path and the launch has no slots left: the lane exits.
+__device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, uint32_t lane, uint32_t& slot,
+                                            uint32_t& res_base, uint32_t& res_left) {
+  const unsigned long long m = __ballot(!in_path);
+  if (m) {
+    const uint32_t need = (uint32_t)__popcll(m);
+    uint32_t fresh = 0;
+    if (res_left < need) {
+      const int leader = __ffsll((long long)m) - 1;
+      if ((int)lane == leader) fresh = atomicAdd(ka.pixel_counter, kClaim);
+      fresh = __shfl(fresh, leader);
+    }
+    if (!in_path) {
+      const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      slot = r < res_left ? res_base + r : fresh + (r - res_left);
+    }
+    if (res_left < need) {
+      res_base = fresh + (need - res_left);
+      res_left = kClaim - (need - res_left);
+    } else {
+      res_base += need;
+      res_left -= need;
+    }
+  }
+  return !in_path && slot >= ka.nsl;
+}
+
 // kCount: the work counters of YK_FLAG_COUNT_WORK (an instance of its own, so the production
 // instance carries neither their registers nor their adds)
-template <bool kSceneInLds, bool kCount>
+// kMode bit 0: the work counters; bit 1: YK_SEED_RANDOM_DEVICE seeding (an instance of its own:
+// the hash's 64-bit arithmetic and two more kernel arguments cost the counter-seeded production
+// instance 0.6% through SGPR spills)
+template <bool kSceneInLds, int kMode>
 __global__ __launch_bounds__(kBlock)
 #if YK_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
 #endif
 void yk_render_persistent(KernelArgs ka) {
+  constexpr bool kCount = (kMode & 1) != 0;
+  constexpr bool kRandomSeed = (kMode & 2) != 0;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -369,40 +410,12 @@ void yk_render_persistent(KernelArgs ka) {
   uint32_t res_base = 0, res_left = 0;
 
   for (;;) {
-    // ---- refill: lanes without a path take the next sample slots from the wave's reserve;
-    //      one atomic per kClaim slots.  Every lane runs this block, so the reserve stays
-    //      uniform.  (A pixel is no longer a lane's unit of work: the samples of a pixel are
-    //      independent, only their SUM is ordered, and that is done by yk_reduce_samples.)
-    {
-      const unsigned long long m = __ballot(!in_path);
-      if (m) {
-        const uint32_t need = (uint32_t)__popcll(m);
-        uint32_t fresh = 0;
-        if (res_left < need) {
-          const int leader = __ffsll((long long)m) - 1;
-          if ((int)lane == leader) fresh = atomicAdd(ka.pixel_counter, kClaim);
-          fresh = __shfl(fresh, leader);
-        }
-        if (!in_path) {
-          const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          slot = r < res_left ? res_base + r : fresh + (r - res_left);
-        }
-        if (res_left < need) {
-          res_base = fresh + (need - res_left);
-          res_left = kClaim - (need - res_left);
-        } else {
-          res_base += need;
-          res_left -= need;
-        }
-      }
-      if (!in_path) {
-        if (slot >= ka.nsl) {
+    // ---- refill (claim_slots): lanes without a path take the next sample slots
+    if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) {
 #if YK_ABLATE & 8
-          atomicMin(&ka.counters[17], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      atomicMin(&ka.counters[17], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
-          break;
-        }
-      }
+      break;
     }
     YK_STAMP(0);
 
@@ -419,7 +432,8 @@ void yk_render_persistent(KernelArgs ka) {
       const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
       const uint32_t y = ka.row_begin + tr * ka.row_stride;
       // seed (uint32 wrap, source.cpp:154-158); x_397 comes from yk_mt_warmup
-      ykd::mt_start_from(g, ka.seed0 + (y * ka.W + x) * ka.spp + s, ka.warm[slot]);
+      ykd::mt_start_from(g, ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s),
+                         ka.warm[slot]);
       // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
       const double u = ykd::div_markstein((double)x + ykd::uniform(g, 0, 1), (double)ka.W, ka.inv_w);
       const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1), (double)ka.H, ka.inv_h);
@@ -748,6 +762,222 @@ void yk_render_persistent(KernelArgs ka) {
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
 
+// The FP64 instance for (scene in LDS, kMode)
+using RenderKernel = void (*)(KernelArgs);
+RenderKernel fp64_kernel(bool lds, int mode) {
+  static const RenderKernel k[8] = {yk_render_persistent<false, 0>, yk_render_persistent<false, 1>,
+                                    yk_render_persistent<false, 2>, yk_render_persistent<false, 3>,
+                                    yk_render_persistent<true, 0>,  yk_render_persistent<true, 1>,
+                                    yk_render_persistent<true, 2>,  yk_render_persistent<true, 3>};
+  return k[(lds ? 4 : 0) + (mode & 3)];
+}
+
+// ---- render<float> (YK_PRECISION_FP32) ---------------------------------------------------
+// The same persistent, sample-parallel structure as yk_render_persistent (refill, slots, MT
+// cursors from yk_mt_warmup, attenuation-id stack, SoA colours reduced by yk_reduce_samples),
+// with the path in float (yk_device_f32.hpp).  Closest hit is the reference's linear scan
+// (hittable_list.hpp:32-58) over float geometry read wave-uniformly (scalar loads): the BVH's
+// culling proof bounds FP64 rounding, not FP32's.
+__device__ __forceinline__ float f_uniform01(ykd::MtLane& g) { return ykf::uniform(g, 0.0f, 1.0f); }
+
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  ykd::MtLane g;
+  g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
+  g.a0 = g.a1 = g.b = g.j = g.seed = 0;
+  uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
+  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_nit = 0, n_ncall = 0;
+  const float tmin = (float)ka.t_min;  // world.hit(r, 0.001, ...) converts to T (hittable.hpp:32)
+  uint32_t slot = 0, depth = 0, nstk = 0;
+  uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+  ykf::v3 o = {0, 0, 0}, d = {0, 0, 0};
+  bool in_path = false;
+  uint32_t res_base = 0, res_left = 0;
+
+  for (;;) {
+    if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) break;
+
+    // ---- start: seed, jitter, camera<float>::get_ray (source.cpp:154-165, camera.hpp:29-32)
+    bool start = !in_path;
+    uint32_t qpix = 0;
+    if (start) {
+      const uint32_t sl = slot / ka.npix_slots;
+      qpix = ka.order[slot - sl * ka.npix_slots];
+      start = qpix != kNoPixel;
+    }
+    if (start) {
+      const uint32_t s = ka.s0 + slot / ka.npix_slots;
+      const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
+      const uint32_t y = ka.row_begin + tr * ka.row_stride;
+      ykd::mt_start_from(g, ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s),
+                         ka.warm[slot]);
+      // (x + U01) / W with x, W unsigned → float (uniform_real_distribution<float>)
+      const float u = ((float)x + f_uniform01(g)) / (float)ka.W;
+      const float v = ((float)(ka.H - y - 1) + f_uniform01(g)) / (float)ka.H;
+      const ykf::v3 cam_o = ykf::of(ka.cam.origin), cam_llc = ykf::of(ka.cam.lower_left_corner);
+      const ykf::v3 cam_h = ykf::of(ka.cam.horizontal), cam_v = ykf::of(ka.cam.vertical);
+      d = ykf::sub(ykf::add(ykf::add(cam_llc, ykf::mul(cam_h, u)), ykf::mul(cam_v, v)), cam_o);
+      o = cam_o;
+      if (ka.cam.lens_radius > 0) {  // thin-lens extension
+        float px, py;
+        do {
+          px = ykf::uniform(g, -1.0f, 1.0f);
+          py = ykf::uniform(g, -1.0f, 1.0f);
+        } while (!(px * px + py * py < 1.0f));
+        const float lr = (float)ka.cam.lens_radius;
+        const float rx = px * lr, ry = py * lr;
+        const ykf::v3 off = ykf::add(ykf::mul(ykf::of(ka.cam.lens_u), rx), ykf::mul(ykf::of(ka.cam.lens_v), ry));
+        o = ykf::add(o, off);
+        d = ykf::sub(d, off);
+      }
+      depth = ka.max_depth;
+      nstk = 0;
+      in_path = true;
+    }
+
+    // ---- closest hit: the reference's ordered scan in float (sphere.hpp:25-48)
+    const bool alive = in_path && depth != 0;
+    float T = INFINITY;
+    int hid = -1;
+    if (alive) {
+      ++n_seg;
+      const float a = ykf::len2(d);
+      for (uint32_t i = 0; i < ka.nspheres; ++i) {
+        const float4 sg = ka.geo_f[i];  // wave-uniform: scalar loads
+        if (kCount) ++n_test;
+        const ykf::v3 oc = {o.x - sg.x, o.y - sg.y, o.z - sg.z};
+        const float hb = ykf::dot(oc, d);
+        const float c = ykf::len2(oc) - sg.w;
+        const float disc = hb * hb - a * c;
+        if (disc < 0) continue;
+        if (kCount) ++n_sqrt, ++n_ncall;
+        const float sq = ykf::nsqrt(disc, n_nit);
+        float root = (-hb - sq) / a;
+        if (root < tmin || T < root) {
+          root = (-hb + sq) / a;
+          if (root < tmin || T < root) continue;
+        }
+        T = root;
+        hid = (int)i;
+      }
+    }
+
+    // ---- shade (raytracer.hpp:25-36, material.hpp) — one normalisation per live lane, as in FP64
+    bool ended = in_path && !alive;
+    double L_r = 0, L_g = 0, L_b = 0;
+    if (alive) {
+      SphereMat m{};
+      ykf::v3 p{0, 0, 0}, nrm{0, 0, 0};
+      bool front = false;
+      ykf::v3 vn = d;
+      if (hid >= 0) {
+        const float4 sg = ka.geo_f[hid];
+        m = ka.mat[hid];
+        p = ykf::add(o, ykf::mul(d, T));  // ray::at
+        const ykf::v3 outward = ykf::divs(ykf::sub(p, ykf::v3{sg.x, sg.y, sg.z}), (float)m.radius);
+        front = ykf::dot(d, outward) < 0;
+        nrm = front ? outward : ykf::neg(outward);
+        if (m.kind == YK_MATERIAL_LAMBERTIAN) vn = ykf::random_vec(g, -1.0f, 1.0f);
+      }
+      if (kCount) ++n_ncall;
+      const ykf::v3 un = ykf::divs(vn, ykf::nsqrt(ykf::len2(vn), n_nit));
+      if (hid < 0) {
+        // sky: normalized(dir).y is a float; + 1.0 and the lerp are double (raytracer.hpp:35-36)
+        const double t = ((double)un.y + 1.0) / 2;
+        L_r = (1.0 - t) * 1.0 + t * 0.5;
+        L_g = (1.0 - t) * 1.0 + t * 0.7;
+        L_b = (1.0 - t) * 1.0 + t * 1.0;
+        ended = true;
+      } else {
+        bool scattered = true, push = true;
+        ykf::v3 nd;
+        if (m.kind == YK_MATERIAL_LAMBERTIAN) {
+          nd = ykf::add(nrm, un);
+          if (ykf::near_zero(nd)) nd = nrm;
+        } else if (m.kind == YK_MATERIAL_METAL) {
+          nd = ykf::reflect(un, nrm);
+          if (m.fuzz > 0) {
+            ykf::v3 ru = ykf::random_vec(g, -1.0f, 1.0f);
+            ru = ykf::divs(ru, ykf::nsqrt(ykf::len2(ru), n_nit));
+            const float k = ykf::uniform(g, 0.01f, 0.99f);
+            nd = ykf::add(nd, ykf::mul(ykf::mul(ru, k), (float)m.fuzz));
+          }
+          scattered = ykf::dot(nd, nrm) > 0;
+        } else {  // dielectric extension, in float
+          push = false;
+          const float ior = (float)m.ior;
+          const float ratio = front ? (1.0f / ior) : ior;
+          float ct = ykf::dot(ykf::neg(un), nrm);
+          if (!(ct < 1.0f)) ct = 1.0f;
+          const float sn = ykf::nsqrt(1.0f - ct * ct, n_nit);
+          const bool cannot = ratio * sn > 1.0f;
+          if (cannot || ykf::reflectance(ct, ratio) > f_uniform01(g)) {
+            nd = ykf::reflect(un, nrm);
+          } else {
+            const ykf::v3 perp = ykf::mul(ykf::add(un, ykf::mul(nrm, ct)), ratio);
+            const float pl = 1.0f - ykf::len2(perp);
+            nd = ykf::add(perp, ykf::mul(nrm, -ykf::nsqrt(pl < 0 ? -pl : pl, n_nit)));
+          }
+        }
+        if (!scattered) {
+          ended = true;
+        } else {
+          if (push) {
+            if (nstk >= kStackRegs) id_spill[nstk - kStackRegs] = (uint16_t)(st3 >> 16);
+            st3 = (st3 << 16) | (st2 >> 16);
+            st2 = (st2 << 16) | (st1 >> 16);
+            st1 = (st1 << 16) | (st0 >> 16);
+            st0 = (st0 << 16) | (uint32_t)hid;
+            ++nstk;
+          }
+          o = p;
+          d = nd;
+          --depth;
+        }
+      }
+    }
+
+    if (ended) {
+      // attenuation (double albedo) back to front, as in FP64 (raytracer.hpp:31)
+      while (nstk > 0) {
+        const uint32_t id = st0 & 0xffffu;
+        st0 = (st0 >> 16) | (st1 << 16);
+        st1 = (st1 >> 16) | (st2 << 16);
+        st2 = (st2 >> 16) | (st3 << 16);
+        st3 = (st3 >> 16) | (nstk > kStackRegs ? ((uint32_t)id_spill[nstk - kStackRegs - 1] << 16) : 0u);
+        --nstk;
+        const SphereMat m = ka.mat[id];
+        L_r = m.ar * L_r;
+        L_g = m.ag * L_g;
+        L_b = m.ab * L_b;
+      }
+      if (ykd::mt_used_fallback(g)) ++n_fb;
+      ka.col[slot] = L_r;
+      ka.col[(size_t)ka.nsl + slot] = L_g;
+      ka.col[2 * (size_t)ka.nsl + slot] = L_b;
+      in_path = false;
+    }
+  }
+  if (kCount) {
+    atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
+    atomicAdd(&ka.counters[1], (unsigned long long)n_test);
+    atomicAdd(&ka.counters[2], (unsigned long long)n_sqrt);
+    atomicAdd(&ka.counters[5], (unsigned long long)n_seg);  // every segment is a linear scan
+    atomicAdd(&ka.counters[6], (unsigned long long)n_ncall);
+    atomicAdd(&ka.counters[7], (unsigned long long)n_nit);
+  }
+  if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
+}
+
+// ykgpu_math_sqrt_f32: the FP32 path's math::sqrt<float> on a buffer (diagnostic).
+__global__ __launch_bounds__(256) void yk_math_sqrt_f32(const float* in, float* out, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t it = 0;
+  if (i < n) out[i] = ykf::nsqrt(in[i], it);
+}
+
 }  // namespace
 
 // =========================================================================================
@@ -756,7 +986,8 @@ void yk_render_persistent(KernelArgs ka) {
 struct ykgpu_context {
   int device = 0;
   int cus = 0;
-  int grid = 0;  // persistent blocks for the current scene
+  int grid = 0;      // persistent blocks for the current scene (FP64 kernel)
+  int grid_f32 = 0;  // persistent blocks of the FP32 kernel
   size_t scratch_lanes = 0;
   bool scene_in_lds = false;
   uint32_t lds_bytes = 0, lds_geo_off = 0, lds_ids_off = 0, lds_stack_off = 0, stack_depth = 0;
@@ -776,6 +1007,7 @@ struct ykgpu_context {
   uint32_t lev_used = 0;
   SphereGeo* d_geo = nullptr;
   SphereMat* d_mat = nullptr;
+  float4* d_geo_f = nullptr;  // FP32 geometry (cx, cy, cz, r*r in float), tuple order
   uint32_t nspheres = 0;
   yk_camera cam{};
   bool have_scene = false;
@@ -812,14 +1044,17 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
     return fail(YK_ERR_INVALID, "row range outside the image");
   if ((uint64_t)p->row_count * p->image_width >= (1ull << 31))
     return fail(YK_ERR_INVALID, "tile larger than 2^31 pixels");
-  if (p->precision != YK_PRECISION_FP64) return fail(YK_ERR_UNSUPPORTED, "precision mode");
+  if (p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32)
+    return fail(YK_ERR_UNSUPPORTED, "precision mode");
   if (p->rng != YK_RNG_MT19937) return fail(YK_ERR_UNSUPPORTED, "rng mode");
+  if (p->seed_mode != YK_SEED_COUNTER && p->seed_mode != YK_SEED_RANDOM_DEVICE)
+    return fail(YK_ERR_UNSUPPORTED, "seed mode");
   if (!(p->t_min >= 0)) return fail(YK_ERR_INVALID, "t_min must be >= 0");
   return YK_OK;
 }
 
-int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth) {
-  const size_t lanes = (size_t)ctx->grid * kBlock;
+int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, int grid) {
+  const size_t lanes = (size_t)grid * kBlock;
   if (lanes > ctx->scratch_lanes) {
     (void)hipFree(ctx->d_mt);
     (void)hipFree(ctx->d_ids);
@@ -886,8 +1121,19 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows) {
 
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
-  int rc = ensure_scratch(ctx, p->max_depth);
+  const bool f32 = p->precision == YK_PRECISION_FP32;
+  const int grid = f32 ? ctx->grid_f32 : ctx->grid;
+  int rc = ensure_scratch(ctx, p->max_depth, grid);
   if (rc) return rc;
+  // YK_SEED_RANDOM_DEVICE without a key: one from std::random_device per call (source.cpp:159)
+  uint64_t seed_key = 0;
+  if (p->seed_mode == YK_SEED_RANDOM_DEVICE) {
+    seed_key = p->seed_key;
+    if (!seed_key) {
+      std::random_device rd;
+      while (!seed_key) seed_key = ((uint64_t)rd() << 32) | rd();
+    }
+  }
   rc = ensure_order(ctx, p->image_width, p->row_count);
   if (rc) return rc;
   // Launch schedule (samples per pixel per launch): 8, 32, 128, ... growing x4 up to the colour
@@ -955,6 +1201,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.leaf_ids = ctx->d_leaf_ids;
   ka.geo = ctx->d_geo;
   ka.mat = ctx->d_mat;
+  ka.geo_f = ctx->d_geo_f;
+  ka.seed_mode = p->seed_mode;
+  ka.seed_key = seed_key;
   ka.pixel_counter = ctx->d_counter;
   ka.mt_scratch = ctx->d_mt;
   ka.id_scratch = ctx->d_ids;
@@ -967,10 +1216,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.row_stride = p->row_stride;
   wa.out = ctx->d_warm;
   wa.npix_slots = nps;
-  wa.pad = 0;
+  wa.seed_mode = p->seed_mode;
+  wa.seed_key = seed_key;
   wa.order = ctx->d_order;
   ka.npix_slots = nps;
-  ka.pad_s = 0;
   ka.pad_n = 0;
   ReduceArgs ra;
   ra.acc = ctx->d_acc;
@@ -1023,14 +1272,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
     YK_HIP(hipEventRecord(ev[2], st));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
-    if (ctx->scene_in_lds && count)
-      hipLaunchKernelGGL((yk_render_persistent<true, true>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
-    else if (ctx->scene_in_lds)
-      hipLaunchKernelGGL((yk_render_persistent<true, false>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
-    else if (count)
-      hipLaunchKernelGGL((yk_render_persistent<false, true>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+    if (f32 && count)
+      hipLaunchKernelGGL((yk_render_f32<true>), dim3(grid), dim3(kBlock), 0, st, ka);
+    else if (f32)
+      hipLaunchKernelGGL((yk_render_f32<false>), dim3(grid), dim3(kBlock), 0, st, ka);
     else
-      hipLaunchKernelGGL((yk_render_persistent<false, false>), dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+      hipLaunchKernelGGL(fp64_kernel(ctx->scene_in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0)),
+                         dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[3], st));
     ra.col = col;
@@ -1051,7 +1299,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ctx->stats = yk_render_stats{};
   ctx->stats.samples = (uint64_t)p->row_count * p->image_width * p->samples_per_pixel;
   ctx->stats.launches = launches;
-  ctx->stats.grid_blocks = (uint32_t)ctx->grid;
+  ctx->stats.grid_blocks = (uint32_t)grid;
+  ctx->stats.seed_key = seed_key;
   ctx->stats_pending = true;
   return YK_OK;
 }
@@ -1126,9 +1375,8 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   auto* ctx = new ykgpu_context();
   ctx->device = device;
   ctx->cus = prop.multiProcessorCount;
-  for (const void* k : {(const void*)yk_render_persistent<true, false>, (const void*)yk_render_persistent<false, false>,
-                        (const void*)yk_render_persistent<true, true>, (const void*)yk_render_persistent<false, true>})
-    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int k8 = 0; k8 < 8; ++k8)
+    (void)hipFuncSetAttribute((const void*)fp64_kernel(k8 & 4, k8 & 3), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
@@ -1148,6 +1396,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   (void)hipFree(ctx->d_geo);
   (void)hipFree(ctx->d_mat);
+  (void)hipFree(ctx->d_geo_f);
   (void)hipFree(ctx->d_counter);
   (void)hipFree(ctx->d_stats);
   (void)hipFree(ctx->d_warm);
@@ -1177,10 +1426,14 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   if (count == 0 || count > 65535) return fail(YK_ERR_INVALID, "sphere count must be 1..65535");
   std::vector<SphereGeo> geo(count);
   std::vector<SphereMat> mat(count);
+  std::vector<float4> geo_f(count);
   for (uint32_t i = 0; i < count; ++i) {
     const yk_sphere& s = spheres[i];
     if (s.material > YK_MATERIAL_DIELECTRIC) return fail(YK_ERR_INVALID, "unknown material kind");
     geo[i] = {s.center[0], s.center[1], s.center[2], s.radius * s.radius};
+    // sphere<float>: centre and radius rounded to float, radius*radius a float product
+    const float rf = (float)s.radius;
+    geo_f[i] = make_float4((float)s.center[0], (float)s.center[1], (float)s.center[2], rf * rf);
     mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0u, 0ull};
   }
   YK_HIP(hipSetDevice(ctx->device));
@@ -1188,12 +1441,16 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   if (count > ctx->nspheres || !ctx->d_geo) {
     (void)hipFree(ctx->d_geo);
     (void)hipFree(ctx->d_mat);
+    (void)hipFree(ctx->d_geo_f);
     ctx->d_geo = nullptr;
     ctx->d_mat = nullptr;
+    ctx->d_geo_f = nullptr;
     YK_HIP(hipMalloc(&ctx->d_geo, count * sizeof(SphereGeo)));
     YK_HIP(hipMalloc(&ctx->d_mat, count * sizeof(SphereMat)));
+    YK_HIP(hipMalloc(&ctx->d_geo_f, count * sizeof(float4)));
   }
   YK_HIP(hipMemcpy(ctx->d_geo, geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
+  YK_HIP(hipMemcpy(ctx->d_geo_f, geo_f.data(), count * sizeof(float4), hipMemcpyHostToDevice));
   // BVH over the spheres (culling only)
   std::vector<double> centers(3 * size_t(count)), radii(count);
   for (uint32_t i = 0; i < count; ++i) {
@@ -1240,10 +1497,14 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   ctx->lds_bytes = ctx->lds_stack_off + ctx->stack_depth * kBlock * (uint32_t)sizeof(int32_t);
   int per_cu = 0;
   hipError_t e = ctx->scene_in_lds
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<true, false>, kBlock, ctx->lds_bytes)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<false, false>, kBlock, ctx->lds_bytes);
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<true, 0>, kBlock, ctx->lds_bytes)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<false, 0>, kBlock, ctx->lds_bytes);
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
   ctx->grid = per_cu * ctx->cus;
+  int per_cu_f = 0;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_f, yk_render_f32<false>, kBlock, 0);
+  if (e != hipSuccess || per_cu_f < 1) per_cu_f = 1;
+  ctx->grid_f32 = per_cu_f * ctx->cus;
   YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));
   ctx->nspheres = count;
   ctx->cam = *camera;
@@ -1320,6 +1581,25 @@ int ykgpu_math_sqrt(ykgpu_context* ctx, const double* in, double* out, uint64_t 
   if (e == hipSuccess) e = hipMemcpy(out, d + n, n * sizeof(double), hipMemcpyDeviceToHost);
   (void)hipFree(d);
   if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_math_sqrt: ") + hipGetErrorString(e));
+  return YK_OK;
+}
+
+int ykgpu_math_sqrt_f32(ykgpu_context* ctx, const float* in, float* out, uint64_t n) {
+  if (!ctx || (n && (!in || !out))) return fail(YK_ERR_INVALID, "null argument");
+  if (n == 0) return YK_OK;
+  YK_HIP(hipSetDevice(ctx->device));
+  float* d = nullptr;
+  YK_HIP(hipMalloc(&d, 2 * n * sizeof(float)));
+  hipError_t e = hipMemcpy(d, in, n * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(yk_math_sqrt_f32, dim3((uint32_t)blocks), dim3(256), 0, ctx->stream, d, d + n, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, d + n, n * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_math_sqrt_f32: ") + hipGetErrorString(e));
   return YK_OK;
 }
 

@@ -13,7 +13,10 @@ MATERIAL_METAL = 1
 MATERIAL_DIELECTRIC = 2
 
 PRECISION_FP64 = 0
+PRECISION_FP32 = 1  # render<float> (include/ykgpu.h)
 RNG_MT19937 = 0
+SEED_COUNTER = 0
+SEED_RANDOM_DEVICE = 1
 FLAG_COUNT_WORK = 1
 FLAG_LINEAR_SCAN = 2
 
@@ -76,8 +79,9 @@ class RenderParams(ctypes.Structure):
         ("precision", ctypes.c_uint32),
         ("rng", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("seed_mode", ctypes.c_uint32),
         ("t_min", ctypes.c_double),
+        ("seed_key", ctypes.c_uint64),
     ]
 
 
@@ -99,6 +103,7 @@ class RenderStats(ctypes.Structure):
         ("phase_cycles", ctypes.c_uint64 * 8),
         ("timeline", ctypes.c_uint64 * 3),
         ("diag", ctypes.c_uint64 * 4),
+        ("seed_key", ctypes.c_uint64),
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
     ]
@@ -113,7 +118,7 @@ class RenderStats(ctypes.Structure):
 
 assert ctypes.sizeof(Sphere) == 80
 assert ctypes.sizeof(Camera) == 19 * 8
-assert ctypes.sizeof(RenderParams) == 56
+assert ctypes.sizeof(RenderParams) == 64
 
 
 def image_height_for(width: int) -> int:
@@ -122,13 +127,14 @@ def image_height_for(width: int) -> int:
 
 
 def make_params(width, height=None, spp=8, max_depth=50, seed0=SEED0_EPOCH0, rows=None,
-                flags=0, t_min=T_MIN) -> RenderParams:
+                flags=0, t_min=T_MIN, precision=PRECISION_FP64, seed_mode=SEED_COUNTER,
+                seed_key=0) -> RenderParams:
     """rows = (row_begin, row_count, row_stride); default: the whole image."""
     if height is None:
         height = image_height_for(width)
     rb, rc, rs = rows if rows is not None else (0, height, 1)
     return RenderParams(width, height, spp, max_depth, seed0 & 0xFFFFFFFF, rb, rc, rs,
-                        PRECISION_FP64, RNG_MT19937, flags, 0, t_min)
+                        precision, RNG_MT19937, flags, seed_mode, t_min, seed_key)
 
 
 def sphere_array(spheres) -> ctypes.Array:
