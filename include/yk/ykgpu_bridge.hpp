@@ -144,6 +144,7 @@ inline void check(int rc, const char* where) {
 // The non-default yk_render_params modes (include/ykgpu.h).
 struct render_options {
   uint32_t precision = YK_PRECISION_FP64;  // YK_PRECISION_FP32: render<float>
+  uint32_t rng = YK_RNG_MT19937;           // YK_RNG_XOR128: yk::xor128 as the per-sample engine
   uint32_t seed_mode = YK_SEED_COUNTER;    // YK_SEED_RANDOM_DEVICE: the runtime build's seeding
   uint64_t seed_key = 0;                   // RANDOM_DEVICE key (0: a fresh one per call)
   double t_min = 0.001;                    // raytracer.hpp:27
@@ -190,7 +191,7 @@ class renderer {
     p.row_count = height;
     p.row_stride = 1;
     p.precision = o.precision;
-    p.rng = YK_RNG_MT19937;
+    p.rng = o.rng;
     p.seed_mode = o.seed_mode;
     p.seed_key = o.seed_key;
     p.t_min = o.t_min;

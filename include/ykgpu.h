@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 3u
+#define YKGPU_ABI_VERSION 4u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 and DIELECTRIC are extensions needed by BASELINE configs 2-5 (no
@@ -53,9 +53,14 @@ enum { YK_MATERIAL_LAMBERTIAN = 0, YK_MATERIAL_METAL = 1, YK_MATERIAL_DIELECTRIC
  * FP32 uses the linear closest-hit scan (the BVH culling proof of DESIGN.md §4 is for FP64). */
 enum { YK_PRECISION_FP64 = 0, YK_PRECISION_FP32 = 1 };
 
-/* Random stream.  MT19937 = yk::mt19937 (random.hpp:148-151) seeded per sample with
- * seed0 + (y*W + x)*spp + s in uint32 arithmetic (source.cpp:154-158). */
-enum { YK_RNG_MT19937 = 0 };
+/* Per-sample engine (the Engine of source.cpp:155/159, seeded per sample as yk_render_params.
+ * seed_mode says).  MT19937 = yk::mt19937 (random.hpp:148-151), render() as shipped.
+ * XOR128 = the reference's other engine, yk::xor128 (random.hpp:18-41: Marsaglia's xorshift128,
+ * x, y, z fixed, w = 88675123 ^ seed), swapped in for yk::mt19937: the fast mode.  Its state is
+ * 4 words, so nothing needs the x_397 warm-up kernel.  (Consecutive counter seeds differ only in
+ * w, so the first draws of neighbouring samples are correlated: that is the engine's, and the
+ * image is the reference's with that engine, bit for bit.) */
+enum { YK_RNG_MT19937 = 0, YK_RNG_XOR128 = 1 };
 
 /* Per-sample seed of the mt19937 (yk_render_params.seed_mode).
  * COUNTER: seed0 + (y*W + x)*spp + s in uint32 arithmetic — the constexpr build

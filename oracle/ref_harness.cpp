@@ -25,6 +25,8 @@
 //   ref_harness samples <scene> W H spp depth seed0 y x s [y x s ...]   (per-sample colours, hex)
 //   ref_harness kat                                                   (RNG / sqrt / canonical KATs)
 //   render32 / samples32: the same with T = float (render<float>(); radius literals as T(...))
+//   render_x128 / samples_x128 / render32_x128 / samples32_x128: the engine is the reference's
+//     yk::xor128 (random.hpp:18-41) seeded with the same per-sample counter, in place of mt19937
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -58,12 +60,13 @@ using L = yk::lambertian<double>;
 using M = yk::metal<double>;
 
 // Counts u32 draws so fixtures can record stream consumption (values are untouched).
+template <class E>
 struct counting_gen {
-  yk::mt19937* g;
+  E* g;
   std::uint64_t n = 0;
-  using result_type = yk::mt19937::result_type;
-  static constexpr result_type min() { return yk::mt19937::min(); }
-  static constexpr result_type max() { return yk::mt19937::max(); }
+  using result_type = typename E::result_type;
+  static constexpr result_type min() { return E::min(); }
+  static constexpr result_type max() { return E::max(); }
   result_type operator()() { ++n; return (*g)(); }
 };
 
@@ -116,13 +119,13 @@ struct job {
 // T = double is render() as shipped (source.cpp:98); T = float is render<float>(): geometry,
 // camera, canonicals (one draw each) and math::sqrt in float, colour still double
 // (raytracer<T, double>, lambertian<double>).
-template <class T, class World>
+template <class T, class E, class World>
 yk::color3d sample_color(const World& world, const job& j, std::uint32_t y, std::uint32_t x,
                          std::uint32_t s, std::uint64_t* draws) {
   const yk::raytracer<T, double> tracer = {};
   const yk::camera<T> cam = {};
-  yk::mt19937 g(j.seed0 + (y * j.W + x) * j.spp + s);
-  counting_gen gen{&g};
+  E g(j.seed0 + (y * j.W + x) * j.spp + s);
+  counting_gen<E> gen{&g};
   yk::uniform_real_distribution<T> dist(0, 1);
   auto u = (x + dist(gen)) / j.W;
   auto v = (j.H - y - 1 + dist(gen)) / j.H;
@@ -131,7 +134,7 @@ yk::color3d sample_color(const World& world, const job& j, std::uint32_t y, std:
   return c;
 }
 
-template <class T, class World>
+template <class T, class E, class World>
 int render(const World& world, const job& j, const char* out_rgb, const char* out_sums) {
   std::vector<unsigned char> rgb(std::size_t(j.W) * j.H * 3);
   std::vector<double> sums(std::size_t(j.W) * j.H * 3);
@@ -140,7 +143,7 @@ int render(const World& world, const job& j, const char* out_rgb, const char* ou
       auto iota = std::views::iota(0u, j.spp);
       yk::color3d pc = std::transform_reduce(
           iota.begin(), iota.end(), yk::color3d(0, 0, 0), std::plus{},
-          [&](auto s) { return sample_color<T>(world, j, y, x, s, nullptr); });
+          [&](auto s) { return sample_color<T, E>(world, j, y, x, s, nullptr); });
       const std::size_t i = std::size_t(y) * j.W + x;
       sums[3 * i + 0] = pc.r;
       sums[3 * i + 1] = pc.g;
@@ -167,7 +170,7 @@ int render(const World& world, const job& j, const char* out_rgb, const char* ou
   return 0;
 }
 
-template <class T, class World>
+template <class T, class E, class World>
 int samples(const World& world, const job& j, int argc, char** argv) {
   std::printf("[\n");
   for (int k = 0; k + 2 < argc; k += 3) {
@@ -175,7 +178,7 @@ int samples(const World& world, const job& j, int argc, char** argv) {
     std::uint32_t x = std::strtoul(argv[k + 1], nullptr, 10);
     std::uint32_t s = std::strtoul(argv[k + 2], nullptr, 10);
     std::uint64_t n = 0;
-    auto c = sample_color<T>(world, j, y, x, s, &n);
+    auto c = sample_color<T, E>(world, j, y, x, s, &n);
     std::printf("  {\"y\": %u, \"x\": %u, \"s\": %u, \"draws\": %llu, \"rgb\": [\"%a\", \"%a\", \"%a\"]}%s\n",
                 y, x, s, (unsigned long long)n, c.r, c.g, c.b, (k + 5 < argc) ? "," : "");
   }
@@ -215,6 +218,24 @@ int kat() {
     }
     std::printf("]%s\n", (k + 1 < sizeof(seeds) / sizeof(seeds[0])) ? "," : "");
   }
+  std::printf("  },\n  \"xor128\": {\n");
+  for (std::size_t k = 0; k < sizeof(seeds) / sizeof(seeds[0]); ++k) {
+    yk::xor128 g(seeds[k]);
+    std::printf("    \"%u\": [", seeds[k]);
+    for (int i = 0; i < 256; ++i) std::printf("%s%llu", i ? ", " : "", (unsigned long long)g());
+    std::printf("]%s\n", (k + 1 < sizeof(seeds) / sizeof(seeds[0])) ? "," : "");
+  }
+  std::printf("  },\n  \"canonical01_x128\": {\n");
+  for (std::size_t k = 0; k < sizeof(seeds) / sizeof(seeds[0]); ++k) {
+    yk::xor128 g(seeds[k]);
+    yk::uniform_real_distribution<double> d01(0, 1), dpm(-1, 1);
+    std::printf("    \"%u\": [", seeds[k]);
+    for (int i = 0; i < 64; ++i) {
+      double v = (i % 3 == 2) ? dpm(g) : d01(g);
+      std::printf("%s\"%a\"", i ? ", " : "", v);
+    }
+    std::printf("]%s\n", (k + 1 < sizeof(seeds) / sizeof(seeds[0])) ? "," : "");
+  }
   std::printf("  },\n  \"newton_sqrt_f32\": [");
   {
     std::vector<float> fs = {0.0f, 1.0f, 2.0f, 4.0f, 0.25f, 1e-30f, 1e-45f, 1e30f, 3.0f, 0.999f, 1e-8f,
@@ -245,18 +266,18 @@ int kat() {
   return 0;
 }
 
-template <class T, class World>
+template <class T, class E, class World>
 int dispatch_world(const World& w, const char* mode, const job& j, int argc, char** argv) {
-  if (!std::strncmp(mode, "render", 6)) return render<T>(w, j, argv[0], argc > 1 ? argv[1] : nullptr);
-  return samples<T>(w, j, argc, argv);
+  if (!std::strncmp(mode, "render", 6)) return render<T, E>(w, j, argv[0], argc > 1 ? argv[1] : nullptr);
+  return samples<T, E>(w, j, argc, argv);
 }
 
-template <class T>
+template <class T, class E>
 int dispatch(const std::string& scene, const char* mode, const job& j, int argc, char** argv) {
-  if (scene == "ref4") return dispatch_world<T>(scene_ref4<T>(), mode, j, argc, argv);
-  if (scene == "lambert3") return dispatch_world<T>(scene_lambert3<T>(), mode, j, argc, argv);
-  if (scene == "mixed12") return dispatch_world<T>(scene_mixed12<T>(), mode, j, argc, argv);
-  if (scene == "walls2") return dispatch_world<T>(scene_walls2<T>(), mode, j, argc, argv);
+  if (scene == "ref4") return dispatch_world<T, E>(scene_ref4<T>(), mode, j, argc, argv);
+  if (scene == "lambert3") return dispatch_world<T, E>(scene_lambert3<T>(), mode, j, argc, argv);
+  if (scene == "mixed12") return dispatch_world<T, E>(scene_mixed12<T>(), mode, j, argc, argv);
+  if (scene == "walls2") return dispatch_world<T, E>(scene_walls2<T>(), mode, j, argc, argv);
   std::fprintf(stderr, "unknown scene %s\n", scene.c_str());
   return 2;
 }
@@ -273,8 +294,13 @@ int main(int argc, char** argv) {
         (std::uint32_t)std::strtoul(argv[5], nullptr, 10), (std::uint32_t)std::strtoul(argv[6], nullptr, 10),
         (std::uint32_t)std::strtoul(argv[7], nullptr, 10)};
   const std::string scene = argv[2];
-  // render32 / samples32: the same loop instantiated with T = float
+  // render32 / samples32: the same loop instantiated with T = float; a "_x128" suffix seeds the
+  // reference's other engine, yk::xor128 (random.hpp:18-41), instead of yk::mt19937
   const bool f32 = std::strstr(argv[1], "32") != nullptr;
-  return f32 ? dispatch<float>(scene, argv[1], j, argc - 8, argv + 8)
-             : dispatch<double>(scene, argv[1], j, argc - 8, argv + 8);
+  const bool x128 = std::strstr(argv[1], "_x128") != nullptr;
+  if (x128)
+    return f32 ? dispatch<float, yk::xor128>(scene, argv[1], j, argc - 8, argv + 8)
+               : dispatch<double, yk::xor128>(scene, argv[1], j, argc - 8, argv + 8);
+  return f32 ? dispatch<float, yk::mt19937>(scene, argv[1], j, argc - 8, argv + 8)
+             : dispatch<double, yk::mt19937>(scene, argv[1], j, argc - 8, argv + 8);
 }

@@ -30,10 +30,14 @@
 #define MT_N 624
 #define MT_M 397
 
+/* The per-sample engine: mt19937 (the reference's, random.hpp:43-151) or, for YK_RNG_XOR128,
+ * the reference's other engine yk::xor128 (random.hpp:18-41) in xs[]. */
 typedef struct {
   uint32_t x[MT_N];
   uint32_t p;
   uint64_t draws;
+  uint32_t kind; /* YK_RNG_* */
+  uint32_t xs[4];
 } mt_t;
 
 /* seed(): random.hpp:69-81 (x_i = 1812433253 * (x_{i-1} ^ x_{i-1} >> 30) + i, mod 2^32) */
@@ -46,6 +50,22 @@ static void mt_seed(mt_t* g, uint32_t sd) {
   }
   g->p = MT_N;
   g->draws = 0;
+  g->kind = YK_RNG_MT19937;
+}
+
+/* xor128(seed): x, y, z at their default member values, w = 88675123 ^ seed (random.hpp:19-32) */
+static void x128_seed(mt_t* g, uint32_t sd) {
+  g->xs[0] = 123456789u;
+  g->xs[1] = 362436069u;
+  g->xs[2] = 521288629u;
+  g->xs[3] = 88675123u ^ sd;
+  g->draws = 0;
+  g->kind = YK_RNG_XOR128;
+}
+
+static void rng_seed(mt_t* g, uint32_t sd, uint32_t kind) {
+  if (kind == YK_RNG_XOR128) x128_seed(g, sd);
+  else mt_seed(g, sd);
 }
 
 static inline uint32_t mt_mix(uint32_t hi_src, uint32_t lo_src) {
@@ -64,6 +84,15 @@ static void mt_twist(mt_t* g) {
 
 /* operator(): random.hpp:95-105 (tempering) */
 static uint32_t mt_next(mt_t* g) {
+  if (g->kind == YK_RNG_XOR128) { /* xor128::operator(), random.hpp:34-40 */
+    uint32_t t = g->xs[0] ^ (g->xs[0] << 11);
+    g->xs[0] = g->xs[1];
+    g->xs[1] = g->xs[2];
+    g->xs[2] = g->xs[3];
+    g->xs[3] = (g->xs[3] ^ (g->xs[3] >> 19)) ^ (t ^ (t >> 8));
+    g->draws++;
+    return g->xs[3];
+  }
   if (g->p >= MT_N) mt_twist(g);
   uint32_t z = g->x[g->p++];
   z ^= (z >> 11);
@@ -144,7 +173,7 @@ static c3 sample(world_t* w, uint32_t y, uint32_t x, uint32_t s, uint64_t* draws
   if (p->seed_mode == YK_SEED_RANDOM_DEVICE)
     seed = seed_from_key(p->seed_key, ((uint64_t)y * p->image_width + x) * p->samples_per_pixel + s);
   if (w->as_shipped) seed = random_device_u32();
-  mt_seed(&g, seed);
+  rng_seed(&g, seed, p->rng);
   c3 c = p->precision == YK_PRECISION_FP32 ? trace_sample_f(w, &g, y, x, segs)
                                            : trace_sample_d(w, &g, y, x, segs);
   if (draws) *draws = g.draws;
@@ -213,7 +242,7 @@ static int check(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_
   if (p->row_count && (p->row_stride == 0 ||
       (uint64_t)p->row_begin + (uint64_t)(p->row_count - 1) * p->row_stride >= p->image_height))
     return YK_ERR_INVALID;
-  if ((p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32) || p->rng != YK_RNG_MT19937 ||
+  if ((p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32) || (p->rng != YK_RNG_MT19937 && p->rng != YK_RNG_XOR128) ||
       p->seed_mode > YK_SEED_RANDOM_DEVICE || (p->seed_mode == YK_SEED_RANDOM_DEVICE && !p->seed_key))
     return YK_ERR_UNSUPPORTED;
   return YK_OK;
@@ -312,3 +341,16 @@ void yko_newton_sqrt_f32_n(const float* in, float* out, uint64_t n) {
 
 /* The per-sample seed of YK_SEED_RANDOM_DEVICE (include/ykgpu.h), for tests. */
 uint32_t yko_seed_from_key(uint64_t key, uint64_t idx) { return seed_from_key(key, idx); }
+
+/* First `count` xor128 outputs for `seed` (random.hpp:18-41), and the KAT canonical pattern. */
+void yko_xor128(uint32_t seed, uint32_t count, uint32_t* out) {
+  mt_t g;
+  x128_seed(&g, seed);
+  for (uint32_t i = 0; i < count; ++i) out[i] = mt_next(&g);
+}
+
+void yko_canonical_pattern_x128(uint32_t seed, uint32_t count, double* out) {
+  mt_t g;
+  x128_seed(&g, seed);
+  for (uint32_t i = 0; i < count; ++i) out[i] = (i % 3 == 2) ? mt_uniform(&g, -1, 1) : mt_uniform(&g, 0, 1);
+}

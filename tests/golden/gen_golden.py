@@ -60,6 +60,22 @@ CASES_F32 = [
     ("ref4", 33, 17, 5, 50, 7, True),
 ]
 
+# yk::xor128 as the per-sample engine (YK_RNG_XOR128): the harness's render_x128 / render32_x128
+CASES_X128 = [
+    ("ref4", 16, 9, 2, 50, 404, True),
+    ("ref4", 200, 112, 8, 50, 404, False),      # config 1 shape
+    ("mixed12", 96, 54, 16, 50, 404, True),
+    ("walls2", 64, 36, 8, 200, 404, True),      # long paths
+    ("ref4", 32, 18, 6, 50, 404, True),
+    ("ref4", 48, 27, 4, 50, 4294967000, True),
+    ("ref4", 33, 17, 5, 50, 7, True),
+]
+CASES_X128_F32 = [
+    ("ref4", 16, 9, 2, 50, 404, True),
+    ("mixed12", 96, 54, 16, 50, 404, True),
+    ("walls2", 64, 36, 8, 200, 404, True),
+]
+
 
 def sha(b: bytes) -> str:
     return hashlib.sha256(b).hexdigest()
@@ -105,8 +121,9 @@ def png_rgb(path):
     return bytes(out), W, H
 
 
-def case_name(scene, W, H, spp, depth, seed0, f32=False):
-    return f"{scene}_{W}x{H}x{spp}_d{depth}_s{seed0}" + ("_f32" if f32 else "")
+def case_name(scene, W, H, spp, depth, seed0, f32=False, x128=False):
+    return (f"{scene}_{W}x{H}x{spp}_d{depth}_s{seed0}" + ("_f32" if f32 else "")
+            + ("_x128" if x128 else ""))
 
 
 def main():
@@ -123,17 +140,21 @@ def main():
     manifest["constexpr_build"] = {"file": "cx16_ref4.rgb", "scene": "ref4", "W": 16, "H": 9,
                                    "spp": 2, "depth": 50, "seed0": 404, "rgb_sha256": sha(rgb)}
 
-    # 2. harness renders (FP64 = render() as shipped, then FP32 = render<float>)
-    for f32, cases in ((False, CASES), (True, CASES_F32)):
+    # 2. harness renders (FP64 = render() as shipped, then FP32 = render<float>; each with
+    #    yk::mt19937 and with yk::xor128 as the engine)
+    for f32, x128, cases in ((False, False, CASES), (True, False, CASES_F32),
+                             (False, True, CASES_X128), (True, True, CASES_X128_F32)):
       for scene, W, H, spp, depth, seed0, keep_sums in cases:
-        name = case_name(scene, W, H, spp, depth, seed0, f32)
+        name = case_name(scene, W, H, spp, depth, seed0, f32, x128)
+        mode = ("render32" if f32 else "render") + ("_x128" if x128 else "")
         with tempfile.TemporaryDirectory() as td:
             f_rgb, f_sums = os.path.join(td, "o.rgb"), os.path.join(td, "o.sums")
-            subprocess.run([HARNESS, "render32" if f32 else "render", scene, str(W), str(H),
+            subprocess.run([HARNESS, mode, scene, str(W), str(H),
                             str(spp), str(depth), str(seed0), f_rgb, f_sums], check=True)
             rgb, sums = open(f_rgb, "rb").read(), open(f_sums, "rb").read()
         entry = {"name": name, "scene": scene, "W": W, "H": H, "spp": spp, "depth": depth,
                  "seed0": seed0, "precision": "fp32" if f32 else "fp64",
+                 "rng": "xor128" if x128 else "mt19937",
                  "rgb_file": name + ".rgb", "rgb_sha256": sha(rgb),
                  "sums_sha256": sha(sums)}
         open(os.path.join(HERE, name + ".rgb"), "wb").write(rgb)
@@ -150,15 +171,18 @@ def main():
     import oracle_lib
     import refscenes
     from uecraytracing_amd.records import make_params
-    from uecraytracing_amd.records import PRECISION_FP32, PRECISION_FP64
-    for scene, W, H, spp, depth, f32 in [("ref4", 200, 112, 8, 50, False),
-                                         ("mixed12", 96, 54, 16, 50, False),
-                                         ("walls2", 64, 36, 8, 200, False),
-                                         ("ref4", 200, 112, 8, 50, True),
-                                         ("walls2", 64, 36, 8, 200, True)]:
+    from uecraytracing_amd.records import PRECISION_FP32, PRECISION_FP64, RNG_MT19937, RNG_XOR128
+    for scene, W, H, spp, depth, f32, x128 in [("ref4", 200, 112, 8, 50, False, False),
+                                               ("mixed12", 96, 54, 16, 50, False, False),
+                                               ("walls2", 64, 36, 8, 200, False, False),
+                                               ("ref4", 200, 112, 8, 50, True, False),
+                                               ("walls2", 64, 36, 8, 200, True, False),
+                                               ("mixed12", 96, 54, 16, 50, False, True),
+                                               ("walls2", 64, 36, 8, 200, False, True)]:
         sph, cam = refscenes.SCENES[scene](), refscenes.reference_camera()
         p = make_params(W, H, spp, depth, 404,
-                        precision=PRECISION_FP32 if f32 else PRECISION_FP64)
+                        precision=PRECISION_FP32 if f32 else PRECISION_FP64,
+                        rng=RNG_XOR128 if x128 else RNG_MT19937)
         cand = []
         for y in range(0, H, 3):
             for x in range(0, W, 5):
@@ -169,12 +193,14 @@ def main():
         pick = cand[:12] + cand[len(cand) // 2:len(cand) // 2 + 6] + cand[-4:]
         pick += [(0, 0, 0, 0), (0, H - 1, W - 1, spp - 1)]
         args = [str(v) for _, y, x, s in pick for v in (y, x, s)]
-        out = subprocess.run([HARNESS, "samples32" if f32 else "samples", scene, str(W), str(H),
+        mode = ("samples32" if f32 else "samples") + ("_x128" if x128 else "")
+        out = subprocess.run([HARNESS, mode, scene, str(W), str(H),
                               str(spp), str(depth), "404"] + args,
                              check=True, capture_output=True, text=True).stdout
-        manifest["samples"][scene + ("_f32" if f32 else "")] = {
+        manifest["samples"][scene + ("_f32" if f32 else "") + ("_x128" if x128 else "")] = {
             "W": W, "H": H, "spp": spp, "depth": depth, "seed0": 404,
-            "precision": "fp32" if f32 else "fp64", "points": json.loads(out)}
+            "precision": "fp32" if f32 else "fp64", "rng": "xor128" if x128 else "mt19937",
+            "points": json.loads(out)}
         print("samples", scene, "max draws", max(e["draws"] for e in json.loads(out)))
 
     # 4. KATs

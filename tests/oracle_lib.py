@@ -49,6 +49,10 @@ def load():
     lib.yko_canonical_pattern_f32.restype = None
     lib.yko_newton_sqrt_f32_n.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     lib.yko_newton_sqrt_f32_n.restype = None
+    lib.yko_xor128.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_uint32)]
+    lib.yko_xor128.restype = None
+    lib.yko_canonical_pattern_x128.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_double)]
+    lib.yko_canonical_pattern_x128.restype = None
     lib.yko_seed_from_key.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
     lib.yko_seed_from_key.restype = ctypes.c_uint32
     _lib = lib
@@ -104,6 +108,19 @@ def sample(spheres, camera, params, y, x, s):
 def mt19937(seed, count):
     out = (ctypes.c_uint32 * count)()
     load().yko_mt19937(seed, count, out)
+    return list(out)
+
+
+def xor128(seed, count):
+    """yk::xor128 (random.hpp:18-41) outputs."""
+    out = (ctypes.c_uint32 * count)()
+    load().yko_xor128(seed, count, out)
+    return list(out)
+
+
+def canonical_pattern_x128(seed, count):
+    out = (ctypes.c_double * count)()
+    load().yko_canonical_pattern_x128(seed, count, out)
     return list(out)
 
 

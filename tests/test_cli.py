@@ -88,6 +88,22 @@ def test_cli_scene_matches_library(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_xor128_matches_reference_golden(tmp_path):
+    """--rng xor128: the reference's yk::xor128 as the engine (harness render_x128 golden)."""
+    out = tmp_path / "x.png"
+    r = run("--width", "16", "--spp", "2", "--seed0", "404", "--rng", "xor128", str(out))
+    assert r.returncode == 0, r.stderr
+    rgb, W, H = golden_data.png_rgb(str(out))
+    e = next(c for c in golden_data.manifest()["cases"] if c["name"] == "ref4_16x9x2_d50_s404_x128")
+    assert golden_data.sha(np.frombuffer(rgb, np.uint8)) == e["rgb_sha256"]
+
+
+def test_cli_rejects_unknown_rng(tmp_path):
+    r = run("--width", "16", "--spp", "1", "--seed0", "1", "--rng", "pcg", str(tmp_path / "o.png"))
+    assert r.returncode == 1 and "unknown rng" in r.stderr
+
+
+@pytest.mark.gpu
 def test_reference_types_drop_in(tmp_path):
     if not os.path.exists(DROPIN):
         pytest.skip("oracle/_ref/ref_dropin not built (needs /root/reference at build time)")

@@ -5,6 +5,9 @@
     float path on the extension scenes; math::sqrt<float> against the reference loop.
   * YK_SEED_RANDOM_DEVICE — per-sample seeds hashed from a per-call key: bit-exact against the
     oracle for a given key; a fresh key per call when none is given, reported in the stats.
+  * YK_RNG_XOR128 — the reference's yk::xor128 as the per-sample engine: bit-exact against the
+    reference-generated *_x128 goldens (test_gpu_parity.test_golden_case) and against the
+    oracle on the extension scenes, the BVH path, row tiles and both precisions.
 """
 import numpy as np
 import pytest
@@ -13,7 +16,7 @@ import golden_data
 import oracle_lib
 import refscenes
 import uecraytracing_amd as yk
-from uecraytracing_amd.records import PRECISION_FP32, SEED_RANDOM_DEVICE, make_params
+from uecraytracing_amd.records import PRECISION_FP32, RNG_XOR128, SEED_RANDOM_DEVICE, make_params
 
 pytestmark = pytest.mark.gpu
 
@@ -122,3 +125,36 @@ def test_random_device_seed_fresh_key_per_call(ren):
     counter = ren.render(make_params(64, 36, 64, 50, 404)).astype(np.float64)
     rnd = ren.render(make_params(64, 36, 64, 50, 0, seed_mode=SEED_RANDOM_DEVICE)).astype(np.float64)
     assert np.sqrt(np.mean(((counter - rnd) / 255.0) ** 2)) < 0.05  # same image, other noise
+
+
+@pytest.mark.parametrize("name,seed,W,H,spp,depth,precision", [
+    ("final", 42, 96, 54, 8, 50, 0),      # 485 spheres: the BVH path with xor128
+    ("glass", 7, 64, 36, 8, 200, 0),      # dielectric-heavy, depth 200 (long paths)
+    ("rtiow5", 0, 80, 45, 8, 50, PRECISION_FP32),
+    ("final", 42, 48, 27, 4, 50, PRECISION_FP32),
+])
+def test_xor128_vs_oracle(ren, name, seed, W, H, spp, depth, precision):
+    arr, cam = yk.build_scene(name, seed)
+    ren.set_scene(arr, cam)
+    p = make_params(W, H, spp, depth, 404, precision=precision, rng=RNG_XOR128)
+    got = ren.render_sums(p)
+    _, want, _, _ = oracle_lib.render(arr, cam, p, want_rgb=False, want_sums=True)
+    assert got.tobytes() == want.tobytes()
+
+
+def test_xor128_row_tiles_random_seed_and_counts(ren):
+    """Row tiles reassemble; the random-device seeding composes with xor128; no MT fallbacks."""
+    arr, cam = yk.build_scene("final", 42)
+    ren.set_scene(arr, cam)
+    W, H = 64, 36
+    full = ren.render(make_params(W, H, 8, 50, 404, rng=RNG_XOR128))
+    out = np.zeros_like(full)
+    for r in range(3):
+        rows = len(range(r, H, 3))
+        out[r::3] = ren.render(make_params(W, H, 8, 50, 404, rows=(r, rows, 3), rng=RNG_XOR128, flags=1))
+        assert ren.stats()["mt_fallbacks"] == 0
+    np.testing.assert_array_equal(out, full)
+    p = make_params(W, H, 4, 50, 0, rng=RNG_XOR128, seed_mode=SEED_RANDOM_DEVICE, seed_key=77)
+    got = ren.render_sums(p)
+    _, want, _, _ = oracle_lib.render(arr, cam, p, want_rgb=False, want_sums=True)
+    assert got.tobytes() == want.tobytes()

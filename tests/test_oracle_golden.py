@@ -9,7 +9,8 @@ import pytest
 import golden_data
 import oracle_lib
 import refscenes
-from uecraytracing_amd.records import PRECISION_FP32, PRECISION_FP64, make_params
+from uecraytracing_amd.records import (PRECISION_FP32, PRECISION_FP64, RNG_MT19937, RNG_XOR128,
+                                       make_params)
 
 MAN = golden_data.manifest()
 CASES = MAN["cases"]
@@ -18,6 +19,24 @@ CASES = MAN["cases"]
 def _precision(spec):
     """fp32 fixtures come from the reference's render<float> (harness render32 mode)."""
     return PRECISION_FP32 if spec.get("precision") == "fp32" else PRECISION_FP64
+
+
+def _rng(spec):
+    """xor128 fixtures come from the harness's *_x128 modes (yk::xor128 as the engine)."""
+    return RNG_XOR128 if spec.get("rng") == "xor128" else RNG_MT19937
+
+
+def test_xor128_kat():
+    """yk::xor128 (random.hpp:18-41) seeded per sample like mt19937: the reference's outputs."""
+    kat = golden_data.kat()["xor128"]
+    for seed, outs in kat.items():
+        assert oracle_lib.xor128(int(seed), len(outs)) == outs, seed
+
+
+def test_canonical_x128_kat():
+    for seed, vals in golden_data.kat()["canonical01_x128"].items():
+        got = oracle_lib.canonical_pattern_x128(int(seed), len(vals))
+        assert [g.hex() for g in got] == [float.fromhex(v).hex() for v in vals], seed
 
 
 def test_mt19937_kat():
@@ -109,7 +128,7 @@ def test_render_matches_reference_large(entry):
 def _check_case(entry):
     sph = refscenes.SCENES[entry["scene"]]()
     p = make_params(entry["W"], entry["H"], entry["spp"], entry["depth"], entry["seed0"],
-                    precision=_precision(entry))
+                    precision=_precision(entry), rng=_rng(entry))
     rgb, sums, _, _ = oracle_lib.render(sph, refscenes.reference_camera(), p, want_sums=True)
     np.testing.assert_array_equal(rgb, golden_data.rgb(entry))
     assert golden_data.sha(sums) == entry["sums_sha256"]
@@ -121,9 +140,9 @@ def _check_case(entry):
 @pytest.mark.parametrize("scene", sorted(MAN["samples"]))
 def test_per_sample_paths(scene):
     spec = MAN["samples"][scene]
-    sph, cam = refscenes.SCENES[scene.removesuffix("_f32")](), refscenes.reference_camera()
+    sph, cam = refscenes.SCENES[spec.get("scene") or scene.split("_")[0]](), refscenes.reference_camera()
     p = make_params(spec["W"], spec["H"], spec["spp"], spec["depth"], spec["seed0"],
-                    precision=_precision(spec))
+                    precision=_precision(spec), rng=_rng(spec))
     for pt in spec["points"]:
         col, draws = oracle_lib.sample(sph, cam, p, pt["y"], pt["x"], pt["s"])
         assert draws == pt["draws"], pt

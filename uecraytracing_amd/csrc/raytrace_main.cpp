@@ -11,11 +11,13 @@
 // reference scene (source.cpp:103-112), built with the same yk calls.
 //
 // Added (render parameters are compile-time macros in the reference): --width, --spp,
-// --depth, --scene, --scene-seed, --scene-file, --save-scene, --seed0, --precision, --device,
-// --stats.  --seed0 fixes the per-sample seed base (seed0 + (y*W+x)*spp + s, the constexpr
+// --depth, --scene, --scene-seed, --scene-file, --save-scene, --seed0, --precision, --rng,
+// --device, --stats.  --seed0 fixes the per-sample seed base (seed0 + (y*W+x)*spp + s, the constexpr
 // build's formula, source.cpp:154-158); without it every sample gets its own seed from a
 // per-call std::random_device key (YK_SEED_RANDOM_DEVICE), like the reference's runtime build
-// (source.cpp:159).  --precision fp32 renders render<float> (T = float, source.cpp:98).
+// (source.cpp:159).  --precision fp32 renders render<float> (T = float, source.cpp:98);
+// --rng xor128 seeds the reference's yk::xor128 (random.hpp:18-41) per sample instead of
+// yk::mt19937.
 // Verbose output: levels 1-2 print the reference's per-pixel / per-sample lines after the GPU
 // render, in the same order; level 3 (per-ray dumps, raytracer.hpp:21-25) is not available.
 #include <cmath>
@@ -67,6 +69,7 @@ const char* kHelp =
     "      --save-scene arg      write the scene to a yk-scene file\n"
     "      --seed0 arg           per-sample seed base (default: random_device)\n"
     "      --precision arg       fp64|fp32: the T of render<T> (default: fp64)\n"
+    "      --rng arg             mt19937|xor128: the per-sample engine (default: mt19937)\n"
     "      --device arg          GPU index (default: 0)\n"
     "      --stats               print kernel time and throughput\n";
 
@@ -80,6 +83,7 @@ struct args {
   bool have_seed0 = false;
   uint32_t seed0 = 0;
   std::string precision = "fp64";
+  std::string rng = "mt19937";
   std::string scene = "ref4";
   std::string scene_file, save_scene;
 };
@@ -132,6 +136,7 @@ args parse(int argc, char** argv) {
       else if (n == "save-scene") a.save_scene = value(i, n, inl);
       else if (n == "seed0") { a.seed0 = to_u32(n, value(i, n, inl)); a.have_seed0 = true; }
       else if (n == "precision") a.precision = value(i, n, inl);
+      else if (n == "rng") a.rng = value(i, n, inl);
       else throw option_error{"Option '" + n + "' does not exist"};
     } else if (s.size() > 1 && s[0] == '-') {
       for (size_t k = 1; k < s.size(); ++k) {
@@ -190,6 +195,12 @@ int main(int argc, char* argv[]) {
     ro.precision = YK_PRECISION_FP32;
   } else if (a.precision != "fp64") {
     std::cerr << "unknown precision " << a.precision << " (fp64|fp32)" << std::endl;
+    return EXIT_FAILURE;
+  }
+  if (a.rng == "xor128") {
+    ro.rng = YK_RNG_XOR128;
+  } else if (a.rng != "mt19937") {
+    std::cerr << "unknown rng " << a.rng << " (mt19937|xor128)" << std::endl;
     return EXIT_FAILURE;
   }
   std::vector<uint8_t> image;

@@ -313,11 +313,39 @@ __device__ __forceinline__ uint32_t sample_seed(uint32_t mode, uint64_t key, uin
   return seed0 + (y * W + x) * spp + s;
 }
 
-// generate_canonical<double,53> (random.hpp:161-183): two draws, sum = u0 + u1*2^32 rounded
-// once, divided by 2^64 (exact), clamped to 1 - eps/2.
-__device__ __forceinline__ double canonical(MtLane& g) {
-  const double u0 = (double)mt_next(g);
-  const double u1 = (double)mt_next(g);
+// yk::xor128 (random.hpp:18-41): Marsaglia's xorshift128, the reference's other engine
+// (YK_RNG_XOR128).  x, y, z start at their default member values and w = 88675123 ^ seed
+// (:19-32); four words of state, so a sample needs neither the x_397 warm-up nor scratch.
+struct X128Lane {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ void x128_start(X128Lane& g, uint32_t seed) {
+  g.x = 123456789u;
+  g.y = 362436069u;
+  g.z = 521288629u;
+  g.w = 88675123u ^ seed;
+}
+__device__ __forceinline__ uint32_t x128_next(X128Lane& g) {  // operator(), :34-40
+  const uint32_t t = g.x ^ (g.x << 11);
+  g.x = g.y;
+  g.y = g.z;
+  g.z = g.w;
+  g.w = (g.w ^ (g.w >> 19)) ^ (t ^ (t >> 8));
+  return g.w;
+}
+__device__ __forceinline__ bool mt_used_fallback(const X128Lane&) { return false; }
+
+// One 32-bit draw of the lane's engine
+__device__ __forceinline__ uint32_t rng_next(MtLane& g) { return mt_next(g); }
+__device__ __forceinline__ uint32_t rng_next(X128Lane& g) { return x128_next(g); }
+
+// generate_canonical<double,53> (random.hpp:161-183): two draws (both engines have
+// min 0, max 2^32-1, so r = 2^32 and m = 2), sum = u0 + u1*2^32 rounded once, divided by 2^64
+// (exact), clamped to 1 - eps/2.
+template <class G>
+__device__ __forceinline__ double canonical(G& g) {
+  const double u0 = (double)rng_next(g);
+  const double u1 = (double)rng_next(g);
   double sum = u0;
   sum = sum + u1 * 4294967296.0;
   double r = sum / 18446744073709551616.0;
@@ -325,11 +353,13 @@ __device__ __forceinline__ double canonical(MtLane& g) {
   return r;
 }
 // uniform_real_distribution::operator() (random.hpp:273-278): c*(b-a)+a
-__device__ __forceinline__ double uniform(MtLane& g, double a, double b) {
+template <class G>
+__device__ __forceinline__ double uniform(G& g, double a, double b) {
   return (canonical(g) * (b - a)) + a;
 }
 // vec3::random(gen, -1, 1) (vec3.hpp:134-142): x, then y, then z
-__device__ __forceinline__ v3 random_vec(MtLane& g, double lo, double hi) {
+template <class G>
+__device__ __forceinline__ v3 random_vec(G& g, double lo, double hi) {
   v3 r;
   r.x = uniform(g, lo, hi);
   r.y = uniform(g, lo, hi);

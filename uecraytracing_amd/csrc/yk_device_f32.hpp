@@ -59,16 +59,19 @@ __device__ __forceinline__ bool near_zero(v3 a) {
 
 // generate_canonical<float, 24> (random.hpp:161-183): m = max(1, (24 + 32) / 33) = 1 draw;
 // sum = float(u) (rounded to nearest), ret = sum / 2^32 (exact scaling), clamped to 1 - eps/2.
-__device__ __forceinline__ float canonical(ykd::MtLane& g) {
-  const float sum = (float)ykd::mt_next(g);
+template <class G>
+__device__ __forceinline__ float canonical(G& g) {
+  const float sum = (float)ykd::rng_next(g);
   float r = sum * 0x1p-32f;
   if (r >= 1.0f) r = 1.0f - 0x1p-24f;
   return r;
 }
 // uniform_real_distribution<float>::operator() (random.hpp:273-278): c*(b-a)+a in float
-__device__ __forceinline__ float uniform(ykd::MtLane& g, float a, float b) { return (ykf::canonical(g) * (b - a)) + a; }
+template <class G>
+__device__ __forceinline__ float uniform(G& g, float a, float b) { return (ykf::canonical(g) * (b - a)) + a; }
 // vec3<float>::random(gen, -1, 1) (vec3.hpp:134-142): x, then y, then z
-__device__ __forceinline__ v3 random_vec(ykd::MtLane& g, float lo, float hi) {
+template <class G>
+__device__ __forceinline__ v3 random_vec(G& g, float lo, float hi) {
   v3 r;
   r.x = ykf::uniform(g, lo, hi);
   r.y = ykf::uniform(g, lo, hi);

@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/ykgpu.h"
@@ -327,6 +328,20 @@ __global__ __launch_bounds__(256) void yk_math_sqrt(const double* in, double* ou
 // res_left) stays wave-uniform.  (A pixel is not a lane's unit of work: the samples of a pixel
 // are independent, only their SUM is ordered, and yk_reduce_samples does that.)  Returns true
 // when this lane has no path and the launch has no slots left: the lane exits.
+// The per-sample engine of a kernel instance (YK_RNG_*): lane set-up and the start of a sample.
+// mt19937 starts from the warm-up kernel's x_397 of the sample slot; xor128 needs only its seed.
+__device__ __forceinline__ void rng_init(ykd::MtLane& g, const KernelArgs& ka, uint32_t gid) {
+  g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
+  g.a0 = g.a1 = g.b = g.j = g.seed = 0;
+}
+__device__ __forceinline__ void rng_init(ykd::X128Lane& g, const KernelArgs&, uint32_t) { g.x = g.y = g.z = g.w = 0; }
+__device__ __forceinline__ void rng_start(ykd::MtLane& g, uint32_t seed, const KernelArgs& ka, uint32_t slot) {
+  ykd::mt_start_from(g, seed, ka.warm[slot]);
+}
+__device__ __forceinline__ void rng_start(ykd::X128Lane& g, uint32_t seed, const KernelArgs&, uint32_t) {
+  ykd::x128_start(g, seed);
+}
+
 __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, uint32_t lane, uint32_t& slot,
                                             uint32_t& res_base, uint32_t& res_left) {
   const unsigned long long m = __ballot(!in_path);
@@ -357,7 +372,7 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
 // instance carries neither their registers nor their adds)
 // kMode bit 0: the work counters; bit 1: YK_SEED_RANDOM_DEVICE seeding (an instance of its own:
 // the hash's 64-bit arithmetic and two more kernel arguments cost the counter-seeded production
-// instance 0.6% through SGPR spills)
+// instance 0.6% through SGPR spills); bit 2: the yk::xor128 engine (YK_RNG_XOR128)
 template <bool kSceneInLds, int kMode>
 __global__ __launch_bounds__(kBlock)
 #if YK_WAVES_PER_EU
@@ -366,6 +381,7 @@ __attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
 void yk_render_persistent(KernelArgs ka) {
   constexpr bool kCount = (kMode & 1) != 0;
   constexpr bool kRandomSeed = (kMode & 2) != 0;
+  using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -389,9 +405,8 @@ void yk_render_persistent(KernelArgs ka) {
   }
   int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlock]
 
-  ykd::MtLane g;
-  g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
-  g.a0 = g.a1 = g.b = g.j = g.seed = 0;
+  Gen g;
+  rng_init(g, ka, gid);
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
 
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0, n_ncall = 0, n_nit = 0;
@@ -431,9 +446,9 @@ void yk_render_persistent(KernelArgs ka) {
       const uint32_t s = ka.s0 + slot / ka.npix_slots;
       const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
       const uint32_t y = ka.row_begin + tr * ka.row_stride;
-      // seed (uint32 wrap, source.cpp:154-158); x_397 comes from yk_mt_warmup
-      ykd::mt_start_from(g, ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s),
-                         ka.warm[slot]);
+      // seed (uint32 wrap, source.cpp:154-158); mt19937's x_397 comes from yk_mt_warmup
+      rng_start(g, ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka,
+                slot);
       // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
       const double u = ykd::div_markstein((double)x + ykd::uniform(g, 0, 1), (double)ka.W, ka.inv_w);
       const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1), (double)ka.H, ka.inv_h);
@@ -765,11 +780,14 @@ void yk_render_persistent(KernelArgs ka) {
 // The FP64 instance for (scene in LDS, kMode)
 using RenderKernel = void (*)(KernelArgs);
 RenderKernel fp64_kernel(bool lds, int mode) {
-  static const RenderKernel k[8] = {yk_render_persistent<false, 0>, yk_render_persistent<false, 1>,
-                                    yk_render_persistent<false, 2>, yk_render_persistent<false, 3>,
-                                    yk_render_persistent<true, 0>,  yk_render_persistent<true, 1>,
-                                    yk_render_persistent<true, 2>,  yk_render_persistent<true, 3>};
-  return k[(lds ? 4 : 0) + (mode & 3)];
+  static const RenderKernel k[16] = {
+      yk_render_persistent<false, 0>, yk_render_persistent<false, 1>, yk_render_persistent<false, 2>,
+      yk_render_persistent<false, 3>, yk_render_persistent<false, 4>, yk_render_persistent<false, 5>,
+      yk_render_persistent<false, 6>, yk_render_persistent<false, 7>, yk_render_persistent<true, 0>,
+      yk_render_persistent<true, 1>,  yk_render_persistent<true, 2>,  yk_render_persistent<true, 3>,
+      yk_render_persistent<true, 4>,  yk_render_persistent<true, 5>,  yk_render_persistent<true, 6>,
+      yk_render_persistent<true, 7>};
+  return k[(lds ? 8 : 0) + (mode & 7)];
 }
 
 // ---- render<float> (YK_PRECISION_FP32) ---------------------------------------------------
@@ -778,15 +796,18 @@ RenderKernel fp64_kernel(bool lds, int mode) {
 // with the path in float (yk_device_f32.hpp).  Closest hit is the reference's linear scan
 // (hittable_list.hpp:32-58) over float geometry read wave-uniformly (scalar loads): the BVH's
 // culling proof bounds FP64 rounding, not FP32's.
-__device__ __forceinline__ float f_uniform01(ykd::MtLane& g) { return ykf::uniform(g, 0.0f, 1.0f); }
+template <class G>
+__device__ __forceinline__ float f_uniform01(G& g) { return ykf::uniform(g, 0.0f, 1.0f); }
 
-template <bool kCount>
+// kMode bit 0: the work counters; bit 2: the yk::xor128 engine (as for the FP64 kernel)
+template <int kMode>
 __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
+  constexpr bool kCount = (kMode & 1) != 0;
+  using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
-  ykd::MtLane g;
-  g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
-  g.a0 = g.a1 = g.b = g.j = g.seed = 0;
+  Gen g;
+  rng_init(g, ka, gid);
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_nit = 0, n_ncall = 0;
   const float tmin = (float)ka.t_min;  // world.hit(r, 0.001, ...) converts to T (hittable.hpp:32)
@@ -811,8 +832,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
       const uint32_t s = ka.s0 + slot / ka.npix_slots;
       const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
       const uint32_t y = ka.row_begin + tr * ka.row_stride;
-      ykd::mt_start_from(g, ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s),
-                         ka.warm[slot]);
+      rng_start(g, ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka, slot);
       // (x + U01) / W with x, W unsigned → float (uniform_real_distribution<float>)
       const float u = ((float)x + f_uniform01(g)) / (float)ka.W;
       const float v = ((float)(ka.H - y - 1) + f_uniform01(g)) / (float)ka.H;
@@ -971,6 +991,11 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
 
+RenderKernel f32_kernel(int mode) {
+  static const RenderKernel k[4] = {yk_render_f32<0>, yk_render_f32<1>, yk_render_f32<4>, yk_render_f32<5>};
+  return k[(mode & 1) | ((mode & 4) >> 1)];
+}
+
 // ykgpu_math_sqrt_f32: the FP32 path's math::sqrt<float> on a buffer (diagnostic).
 __global__ __launch_bounds__(256) void yk_math_sqrt_f32(const float* in, float* out, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1022,6 +1047,7 @@ struct ykgpu_context {
   uint32_t* d_mt = nullptr;             // grid*256*624 words
   uint16_t* d_ids = nullptr;            // grid*256*id_stride
   uint32_t id_stride = 0;
+  size_t id_lanes = 0;
   uint8_t* d_rgb = nullptr;
   size_t rgb_cap = 0;
   double* d_sums = nullptr;
@@ -1046,30 +1072,33 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
     return fail(YK_ERR_INVALID, "tile larger than 2^31 pixels");
   if (p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32)
     return fail(YK_ERR_UNSUPPORTED, "precision mode");
-  if (p->rng != YK_RNG_MT19937) return fail(YK_ERR_UNSUPPORTED, "rng mode");
+  if (p->rng != YK_RNG_MT19937 && p->rng != YK_RNG_XOR128) return fail(YK_ERR_UNSUPPORTED, "rng mode");
   if (p->seed_mode != YK_SEED_COUNTER && p->seed_mode != YK_SEED_RANDOM_DEVICE)
     return fail(YK_ERR_UNSUPPORTED, "seed mode");
   if (!(p->t_min >= 0)) return fail(YK_ERR_INVALID, "t_min must be >= 0");
   return YK_OK;
 }
 
-int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, int grid) {
+int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, int grid, bool need_mt) {
   const size_t lanes = (size_t)grid * kBlock;
-  if (lanes > ctx->scratch_lanes) {
+  // mt19937 fallback engines: 624 words per persistent lane (not needed by xor128)
+  if (need_mt && (lanes > ctx->scratch_lanes || !ctx->d_mt)) {
     (void)hipFree(ctx->d_mt);
-    (void)hipFree(ctx->d_ids);
     ctx->d_mt = nullptr;
-    ctx->d_ids = nullptr;
-    ctx->id_stride = 0;
+    ctx->scratch_lanes = 0;
     YK_HIP(hipMalloc(&ctx->d_mt, lanes * ykd::kMtN * sizeof(uint32_t)));
     ctx->scratch_lanes = lanes;
   }
+  // attenuation-id spill: max_depth u16 per lane
   const uint32_t need = max_depth > kStackRegs ? max_depth : 1;
-  if (need > ctx->id_stride || !ctx->d_ids) {
+  if (need > ctx->id_stride || lanes > ctx->id_lanes || !ctx->d_ids) {
     if (ctx->d_ids) YK_HIP(hipFree(ctx->d_ids));
     ctx->d_ids = nullptr;
+    ctx->id_stride = 0;
+    ctx->id_lanes = 0;
     YK_HIP(hipMalloc(&ctx->d_ids, lanes * need * sizeof(uint16_t)));
     ctx->id_stride = need;
+    ctx->id_lanes = lanes;
   }
   return YK_OK;
 }
@@ -1122,8 +1151,9 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows) {
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
   const bool f32 = p->precision == YK_PRECISION_FP32;
+  const bool x128 = p->rng == YK_RNG_XOR128;  // no x_397 warm-ups, no MT scratch
   const int grid = f32 ? ctx->grid_f32 : ctx->grid;
-  int rc = ensure_scratch(ctx, p->max_depth, grid);
+  int rc = ensure_scratch(ctx, p->max_depth, grid, !x128);
   if (rc) return rc;
   // YK_SEED_RANDOM_DEVICE without a key: one from std::random_device per call (source.cpp:159)
   uint64_t seed_key = 0;
@@ -1167,7 +1197,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const uint32_t nlaunch = (uint32_t)sched.size();
   const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (4ull * nps * K)));
-  if ((rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K, sizeof(uint32_t)))) return rc;
+  if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K, sizeof(uint32_t)))) return rc;
   // two colour buffers: reduce c (stream red) overlaps render c + 1
   if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)2 * nps * K * 3, sizeof(double)))) return rc;
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
@@ -1250,8 +1280,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * 32);
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
-    hipLaunchKernelGGL(yk_mt_warmup, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
-    YK_HIP(hipGetLastError());
+    if (!x128) {
+      hipLaunchKernelGGL(yk_mt_warmup, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      YK_HIP(hipGetLastError());
+    }
     YK_HIP(hipEventRecord(ev[1], ctx->aux));
     return YK_OK;
   };
@@ -1266,18 +1298,17 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.s0 = s0;
     ka.nsl = nsl;
     ka.col = col;
-    ka.warm = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
+    ka.warm = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
     YK_HIP(hipStreamWaitEvent(st, ev[1], 0));                                // its x_397
     if (c >= 2) YK_HIP(hipStreamWaitEvent(st, ctx->lev[6 * (c - 2) + 5], 0));  // its colour buffer
     YK_HIP(hipMemsetAsync(ctx->d_counter, 0, 16, st));
     YK_HIP(hipEventRecord(ev[2], st));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
-    if (f32 && count)
-      hipLaunchKernelGGL((yk_render_f32<true>), dim3(grid), dim3(kBlock), 0, st, ka);
-    else if (f32)
-      hipLaunchKernelGGL((yk_render_f32<false>), dim3(grid), dim3(kBlock), 0, st, ka);
+    if (f32)
+      hipLaunchKernelGGL(f32_kernel((count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(kBlock), 0, st, ka);
     else
-      hipLaunchKernelGGL(fp64_kernel(ctx->scene_in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0)),
+      hipLaunchKernelGGL(fp64_kernel(ctx->scene_in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
+                                                            (x128 ? 4 : 0)),
                          dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[3], st));
@@ -1375,8 +1406,9 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   auto* ctx = new ykgpu_context();
   ctx->device = device;
   ctx->cus = prop.multiProcessorCount;
-  for (int k8 = 0; k8 < 8; ++k8)
-    (void)hipFuncSetAttribute((const void*)fp64_kernel(k8 & 4, k8 & 3), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int k16 = 0; k16 < 16; ++k16)
+    (void)hipFuncSetAttribute((const void*)fp64_kernel(k16 & 8, k16 & 7), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
@@ -1502,7 +1534,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   if (e != hipSuccess || per_cu < 1) per_cu = 1;
   ctx->grid = per_cu * ctx->cus;
   int per_cu_f = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_f, yk_render_f32<false>, kBlock, 0);
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_f, yk_render_f32<0>, kBlock, 0);
   if (e != hipSuccess || per_cu_f < 1) per_cu_f = 1;
   ctx->grid_f32 = per_cu_f * ctx->cus;
   YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));

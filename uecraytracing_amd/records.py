@@ -15,6 +15,7 @@ MATERIAL_DIELECTRIC = 2
 PRECISION_FP64 = 0
 PRECISION_FP32 = 1  # render<float> (include/ykgpu.h)
 RNG_MT19937 = 0
+RNG_XOR128 = 1  # yk::xor128 (random.hpp:18-41), the fast mode (include/ykgpu.h)
 SEED_COUNTER = 0
 SEED_RANDOM_DEVICE = 1
 FLAG_COUNT_WORK = 1
@@ -128,13 +129,13 @@ def image_height_for(width: int) -> int:
 
 def make_params(width, height=None, spp=8, max_depth=50, seed0=SEED0_EPOCH0, rows=None,
                 flags=0, t_min=T_MIN, precision=PRECISION_FP64, seed_mode=SEED_COUNTER,
-                seed_key=0) -> RenderParams:
+                seed_key=0, rng=RNG_MT19937) -> RenderParams:
     """rows = (row_begin, row_count, row_stride); default: the whole image."""
     if height is None:
         height = image_height_for(width)
     rb, rc, rs = rows if rows is not None else (0, height, 1)
     return RenderParams(width, height, spp, max_depth, seed0 & 0xFFFFFFFF, rb, rc, rs,
-                        precision, RNG_MT19937, flags, seed_mode, t_min, seed_key)
+                        precision, rng, flags, seed_mode, t_min, seed_key)
 
 
 def sphere_array(spheres) -> ctypes.Array:
