@@ -181,4 +181,73 @@ std::vector<SlabNode> slab_nodes(const Built& b) {
 
 int32_t slab_root(const Built& b) { return slab_code(b.root); }
 
+namespace {
+struct Slot {
+  float lo[3], hi[3];
+  int32_t code;  // binary-tree code: >= 0 inner node index, < 0 leaf
+};
+
+float slot_area(const Slot& e) {
+  const float dx = e.hi[0] - e.lo[0], dy = e.hi[1] - e.lo[1], dz = e.hi[2] - e.lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+Slot child_slot(const Node& n, int k) {
+  return Slot{{n.lo_x[k], n.lo_y[k], n.lo_z[k]}, {n.hi_x[k], n.hi_y[k], n.hi_z[k]}, n.child[k]};
+}
+
+// Emits the wide node for binary inner node `idx` (and its subtree) into out; returns its index.
+uint32_t collapse(const Built& b, int32_t idx, std::vector<WideNode>& out, uint32_t depth, uint32_t& max_depth) {
+  std::vector<Slot> slots = {child_slot(b.nodes[idx], 0), child_slot(b.nodes[idx], 1)};
+  while (slots.size() < 4) {
+    int best = -1;
+    for (size_t i = 0; i < slots.size(); ++i)
+      if (slots[i].code >= 0 && (best < 0 || slot_area(slots[i]) > slot_area(slots[best]))) best = (int)i;
+    if (best < 0) break;
+    const Node& c = b.nodes[slots[best].code];
+    slots[best] = child_slot(c, 0);
+    slots.insert(slots.begin() + best + 1, child_slot(c, 1));  // siblings stay adjacent
+  }
+  max_depth = std::max(max_depth, depth + 1);
+  const uint32_t me = (uint32_t)out.size();
+  out.emplace_back();
+  int32_t codes[4];
+  for (int k = 0; k < 4; ++k) {
+    if (k >= (int)slots.size()) {
+      codes[k] = kEmptyLeaf;
+    } else if (slots[k].code >= 0) {
+      codes[k] = (int32_t)(collapse(b, slots[k].code, out, depth + 1, max_depth) * sizeof(WideNode));
+    } else {
+      codes[k] = slots[k].code;
+    }
+  }
+  WideNode& w = out[me];
+  float* ax[3] = {w.x, w.y, w.z};
+  for (int k = 0; k < 4; ++k) {
+    const bool used = k < (int)slots.size();
+    for (int a = 0; a < 3; ++a) {
+      const float lo = used ? slots[k].lo[a] : 3e38f, hi = used ? slots[k].hi[a] : -3e38f;
+      ax[a][k] = lo;
+      ax[a][4 + k] = hi;
+      ax[a][8 + k] = lo;
+    }
+    w.child[k] = codes[k];
+  }
+  return me;
+}
+}  // namespace
+
+std::vector<WideNode> wide_nodes(const Built& b, int32_t* root_code, uint32_t* wide_depth) {
+  std::vector<WideNode> out;
+  uint32_t depth = 0;
+  if (b.root >= 0) {
+    collapse(b, b.root, out, 0, depth);
+    *root_code = 0;
+  } else {
+    *root_code = b.root;  // a single leaf
+  }
+  *wide_depth = depth;
+  return out;
+}
+
 }  // namespace ykbvh

@@ -40,6 +40,21 @@ struct alignas(16) SlabNode {
 };
 static_assert(sizeof(SlabNode) == 80, "SlabNode layout");
 
+// 4-wide device node (160 bytes), built by wide_nodes() by collapsing the binary tree: each slot
+// whose child is an inner node is replaced by that node's two children, the largest surface
+// area first, until the node has 4 slots or only leaves.  Per axis, the 4 slots' planes as
+// [lo x4][hi x4][lo x4]: a ray with 1/d >= 0 reads (near x4, far x4) at bytes (0, 16) of the
+// axis, a ray with 1/d < 0 at (16, 32) — the SlabNode trick with 16-byte reads.  child >= 0 is
+// the BYTE OFFSET of an inner WideNode, < 0 a leaf code; an unused slot has an empty box
+// (lo = +3e38, hi = -3e38: near > far for any ray) and the empty leaf code ~0 (no spheres).
+// The culling per slot is the binary node's (same planes, same rounding): DESIGN.md §4 holds.
+struct alignas(16) WideNode {
+  float x[12], y[12], z[12];
+  int32_t child[4];
+};
+static_assert(sizeof(WideNode) == 160, "WideNode layout");
+constexpr int32_t kEmptyLeaf = ~0;  // leaf code with no spheres
+
 struct Built {
   std::vector<Node> nodes;      // nodes[0] is the root when root >= 0
   std::vector<uint32_t> order;  // leaf slots → original sphere index (tuple order)
@@ -60,6 +75,9 @@ Built build(const double* centers, const double* radii, uint32_t n, double camer
 // Nodes in SlabNode layout, and the root code in that encoding (byte offset or leaf code).
 std::vector<SlabNode> slab_nodes(const Built& b);
 int32_t slab_root(const Built& b);
+// 4-wide nodes (DFS order, root first), the root code in that encoding, and the wide depth
+// (inner nodes on the longest root-to-leaf path).
+std::vector<WideNode> wide_nodes(const Built& b, int32_t* root_code, uint32_t* wide_depth);
 constexpr uint32_t kMaxDepth = 32;  // traversal stack capacity (device, LDS)
 
 }  // namespace ykbvh

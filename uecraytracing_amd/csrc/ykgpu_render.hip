@@ -79,6 +79,15 @@ static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 #define YK_WAVES_PER_EU 0
 #endif
 constexpr int kBlock = YK_BLOCK;
+// YK_WIDE: 4-wide BVH nodes (ykbvh::WideNode); 0 = the binary slab nodes (A/B timing)
+#ifndef YK_WIDE
+#define YK_WIDE 1
+#endif
+#if YK_WIDE
+using DevNode = ykbvh::WideNode;
+#else
+using DevNode = ykbvh::SlabNode;
+#endif
 constexpr int kCounters = 24;  // [16..18]: timeline, [19..22]: diag (diagnostic builds)
 
 // Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
@@ -121,8 +130,8 @@ struct KernelArgs {
   double origin_bound;  // |o|_inf beyond which the BVH's float culling is not proven sound
   int32_t bvh_root;
   uint32_t n_nodes;
-  uint32_t lds_geo_off, lds_ids_off, lds_stack_off, stack_depth;
-  const ykbvh::SlabNode* __restrict__ nodes;  // child links are byte offsets from nodes
+  uint32_t lds_geo_off, lds_ids_off, lds_stack_off, stack_cap;  // stack_cap: entries a lane may hold
+  const DevNode* __restrict__ nodes;  // child links are byte offsets from nodes
   const SphereGeo* __restrict__ leaf_geo;  // spheres in BVH leaf order
   const uint32_t* __restrict__ leaf_ids;   // leaf slot → tuple index
   const SphereGeo* __restrict__ geo;
@@ -172,6 +181,7 @@ __device__ __noinline__ Hit scan_linear(const SphereGeo* __restrict__ geo, uint3
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float safe_rcp(float x) {
   return fabsf(x) > 1e-30f ? 1.0f / x : copysignf(1e30f, x);
@@ -391,7 +401,7 @@ void yk_render_persistent(KernelArgs ka) {
   if (kSceneInLds) {
     const uint4* src[3] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids};
     const uint32_t off[3] = {0u, ka.lds_geo_off, ka.lds_ids_off};
-    const uint32_t n16[3] = {(ka.n_nodes * (uint32_t)sizeof(ykbvh::SlabNode) + 15u) / 16u, ka.nspheres * 2u,
+    const uint32_t n16[3] = {(ka.n_nodes * (uint32_t)sizeof(DevNode) + 15u) / 16u, ka.nspheres * 2u,
                              (ka.nspheres + 3u) / 4u};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -497,11 +507,19 @@ void yk_render_persistent(KernelArgs ka) {
         // arithmetic only, so explicit FMAs are fine here.
         const float ix = safe_rcp((float)d.x), iy = safe_rcp((float)d.y), iz = safe_rcp((float)d.z);
         const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
+#if YK_WIDE
+        // this ray's (near x4, far x4) plane quads inside a WideNode (yk_bvh.hpp), as base
+        // pointers: a visit then costs one address add per axis
+        const char* const px = nodes + (ix < 0.0f ? 16u : 0u);
+        const char* const py = nodes + 48u + (iy < 0.0f ? 16u : 0u);
+        const char* const pz = nodes + 96u + (iz < 0.0f ? 16u : 0u);
+#else
         // this ray's (near, far) plane pairs inside a SlabNode (yk_bvh.hpp), as base pointers:
         // a visit then costs one address add per axis
         const char* const px = nodes + (ix < 0.0f ? 8u : 0u);
         const char* const py = nodes + 24u + (iy < 0.0f ? 8u : 0u);
         const char* const pz = nodes + 48u + (iz < 0.0f ? 8u : 0u);
+#endif
         // Conservative interval test without per-visit relaxation: far distances
         // come out of the FMA already scaled by c = 1 + 2^-17 (scaled 1/d and o/d), near
         // distances are compared unscaled against tmin_lo = t_min (1 - 2^-17) and against
@@ -542,6 +560,46 @@ void yk_render_persistent(KernelArgs ka) {
             // lane counts
             if ((uint32_t)__builtin_ctzll(__ballot(1)) == lane) ++st_acc[7];
 #endif
+#if YK_WIDE
+            // near / far distances of the 4 slots per axis, one packed FMA per pair of slots:
+            // t = plane*(1/d) - o*(1/d), the binary node's arithmetic per slot
+            const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
+            const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
+            const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
+            const int4 ch = *(const int4*)(nodes + node + 144);
+            const f2 nx[2] = {__builtin_elementwise_fma(qnx.xy, ixv, noix), __builtin_elementwise_fma(qnx.zw, ixv, noix)};
+            const f2 fx[2] = {__builtin_elementwise_fma(qfx.xy, ixc, noixc), __builtin_elementwise_fma(qfx.zw, ixc, noixc)};
+            const f2 ny[2] = {__builtin_elementwise_fma(qny.xy, iyv, noiy), __builtin_elementwise_fma(qny.zw, iyv, noiy)};
+            const f2 fy[2] = {__builtin_elementwise_fma(qfy.xy, iyc, noiyc), __builtin_elementwise_fma(qfy.zw, iyc, noiyc)};
+            const f2 nz[2] = {__builtin_elementwise_fma(qnz.xy, izv, noiz), __builtin_elementwise_fma(qnz.zw, izv, noiz)};
+            const f2 fz[2] = {__builtin_elementwise_fma(qfz.xy, izc, noizc), __builtin_elementwise_fma(qfz.zw, izc, noizc)};
+            bool hk[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float tn = fmaxf(fmaxf(fmaxf(nx[k >> 1][k & 1], ny[k >> 1][k & 1]), nz[k >> 1][k & 1]), tmin_lo);
+              const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
+              hk[k] = tn <= tf;
+            }
+            if (hk[0] || hk[1] || hk[2] || hk[3]) {
+              // the last slot entered is visited next and the others entered are pushed, in slot
+              // order: no distance sort (visit order only affects how fast U* shrinks, never the
+              // result; modelled by tools/bvhsim, it costs ~1% more leaf tests and no node
+              // visits).  Each write lands at the current top, which moves only for a push.
+              node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : ch.x));
+              stk[sp * kBlock] = ch.x;
+              sp += (hk[0] && (hk[1] || hk[2] || hk[3])) ? 1u : 0u;
+              stk[sp * kBlock] = ch.y;
+              sp += (hk[1] && (hk[2] || hk[3])) ? 1u : 0u;
+              stk[sp * kBlock] = ch.z;
+              sp += (hk[2] && hk[3]) ? 1u : 0u;
+              if (sp > ka.stack_cap) {  // stack full: abandon, the exact linear scan decides
+                overflow = true;
+                sp = 0;
+                node = ykbvh::kEmptyLeaf;
+              }
+              continue;
+            }
+#else
             // near / far distances of both children per axis, one packed FMA per pair:
             // t = plane*(1/d) - o*(1/d)
             const char* const ax = px + node;
@@ -572,6 +630,7 @@ void yk_render_persistent(KernelArgs ka) {
               node = h0 ? ch.x : ch.y;
               continue;
             }
+#endif
           } else {
             YK_STAMP(2);  // interior nodes since the last stamp
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
@@ -1015,7 +1074,7 @@ struct ykgpu_context {
   int grid_f32 = 0;  // persistent blocks of the FP32 kernel
   size_t scratch_lanes = 0;
   bool scene_in_lds = false;
-  uint32_t lds_bytes = 0, lds_geo_off = 0, lds_ids_off = 0, lds_stack_off = 0, stack_depth = 0;
+  uint32_t lds_bytes = 0, lds_geo_off = 0, lds_ids_off = 0, lds_stack_off = 0, stack_entries = 0, stack_cap = 0;
   uint32_t n_nodes = 0;
   uint32_t* d_warm = nullptr;  // x_397 per sample slot of one launch
   double* d_col = nullptr;     // sample colours of one launch (SoA)
@@ -1038,7 +1097,7 @@ struct ykgpu_context {
   bool have_scene = false;
   uint32_t* d_counter = nullptr;        // [0] pixel counter
   unsigned long long* d_stats = nullptr;  // kCounters counters
-  ykbvh::SlabNode* d_nodes = nullptr;
+  DevNode* d_nodes = nullptr;
   SphereGeo* d_leaf_geo = nullptr;
   uint32_t* d_leaf_ids = nullptr;
   int32_t bvh_root = 0;
@@ -1225,7 +1284,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.lds_geo_off = ctx->lds_geo_off;
   ka.lds_ids_off = ctx->lds_ids_off;
   ka.lds_stack_off = ctx->lds_stack_off;
-  ka.stack_depth = ctx->stack_depth;
+  ka.stack_cap = ctx->stack_cap;
   ka.nodes = ctx->d_nodes;
   ka.leaf_geo = ctx->d_leaf_geo;
   ka.leaf_ids = ctx->d_leaf_ids;
@@ -1503,30 +1562,54 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   ctx->d_nodes = nullptr;
   ctx->d_leaf_geo = nullptr;
   ctx->d_leaf_ids = nullptr;
-  const std::vector<ykbvh::SlabNode> snodes = ykbvh::slab_nodes(bvh);
+#if YK_WIDE
+  int32_t root_code = 0;
+  uint32_t wdepth = 0;
+  const std::vector<DevNode> snodes = ykbvh::wide_nodes(bvh, &root_code, &wdepth);
+#else
+  const std::vector<DevNode> snodes = ykbvh::slab_nodes(bvh);
+  const int32_t root_code = ykbvh::slab_root(bvh);
+#endif
   const size_t nn = std::max<size_t>(1, snodes.size());
-  YK_HIP(hipMalloc(&ctx->d_nodes, nn * sizeof(ykbvh::SlabNode)));
+  YK_HIP(hipMalloc(&ctx->d_nodes, nn * sizeof(DevNode)));
   YK_HIP(hipMalloc(&ctx->d_leaf_geo, count * sizeof(SphereGeo)));
   YK_HIP(hipMalloc(&ctx->d_leaf_ids, count * sizeof(uint32_t)));
   if (!snodes.empty())
-    YK_HIP(hipMemcpy(ctx->d_nodes, snodes.data(), snodes.size() * sizeof(ykbvh::SlabNode),
+    YK_HIP(hipMemcpy(ctx->d_nodes, snodes.data(), snodes.size() * sizeof(DevNode),
                      hipMemcpyHostToDevice));
   YK_HIP(hipMemcpy(ctx->d_leaf_geo, leaf_geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
   YK_HIP(hipMemcpy(ctx->d_leaf_ids, bvh.order.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
-  ctx->bvh_root = ykbvh::slab_root(bvh);
+  ctx->bvh_root = root_code;
   ctx->bvh_depth = bvh.depth;
   ctx->origin_bound = bvh.origin_bound;
-  ctx->n_nodes = (uint32_t)bvh.nodes.size();
+  ctx->n_nodes = (uint32_t)snodes.size();
   // LDS layout: [nodes][leaf geometry][leaf ids][traversal stacks]
   auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  const size_t scene_bytes = a16(ctx->n_nodes * sizeof(ykbvh::SlabNode)) + a16(count * sizeof(SphereGeo)) +
+  const size_t scene_bytes = a16(ctx->n_nodes * sizeof(DevNode)) + a16(count * sizeof(SphereGeo)) +
                              a16(count * sizeof(uint32_t));
   ctx->scene_in_lds = scene_bytes <= 64 * 1024;
-  ctx->stack_depth = bvh.depth + 1;
-  ctx->lds_geo_off = (uint32_t)a16(ctx->n_nodes * sizeof(ykbvh::SlabNode));
+#if YK_WIDE
+  // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries), but
+  // the stacks share LDS with the scene, so the capacity is what still fits 3 blocks per CU (at
+  // least 8); a lane that would exceed it abandons the traversal for the exact linear scan.
+  // Pushes write unconditionally at the current top (up to 3 past the capacity): +4 entries.
+  {
+    // (2 KB below a third of the CU's LDS: the hardware's allocation granularity — 3 blocks of
+    // 54144 bytes measured only 2 resident per CU, with the grid still sized for 3)
+    const size_t budget = (size_t)160 * 1024 / 3 - 2048;
+    const size_t used = ctx->scene_in_lds ? scene_bytes : 0;
+    const uint32_t fit = used + 12 * kBlock * 4 <= budget ? (uint32_t)((budget - used) / (kBlock * 4)) : 12u;
+    ctx->stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
+    ctx->stack_entries = ctx->stack_cap + 4;
+  }
+#else
+  ctx->stack_cap = bvh.depth + 1;
+  ctx->stack_entries = bvh.depth + 1;
+#endif
+  ctx->lds_geo_off = (uint32_t)a16(ctx->n_nodes * sizeof(DevNode));
   ctx->lds_ids_off = ctx->lds_geo_off + (uint32_t)a16(count * sizeof(SphereGeo));
   ctx->lds_stack_off = ctx->scene_in_lds ? (uint32_t)scene_bytes : 0u;
-  ctx->lds_bytes = ctx->lds_stack_off + ctx->stack_depth * kBlock * (uint32_t)sizeof(int32_t);
+  ctx->lds_bytes = ctx->lds_stack_off + ctx->stack_entries * kBlock * (uint32_t)sizeof(int32_t);
   int per_cu = 0;
   hipError_t e = ctx->scene_in_lds
       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<true, 0>, kBlock, ctx->lds_bytes)
