@@ -547,7 +547,12 @@ void yk_render_persistent(KernelArgs ka) {
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
         bool overflow = false;
         int32_t node = ka.bvh_root;
+#if YK_WIDE
+        int32_t* top = stk;  // this lane's traversal stack top (entries kBlock words apart)
+        const int32_t* const stk_cap = stk + ka.stack_cap * kBlock;
+#else
         uint32_t sp = 0;
+#endif
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
@@ -580,21 +585,24 @@ void yk_render_persistent(KernelArgs ka) {
               const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
+            // keep the child-code read in this block, issued with the plane reads (the compiler
+            // would otherwise sink it into the branch below and wait for it there)
+            asm volatile("" ::"v"(ch.x), "v"(ch.y), "v"(ch.z), "v"(ch.w));
             if (hk[0] || hk[1] || hk[2] || hk[3]) {
               // the last slot entered is visited next and the others entered are pushed, in slot
               // order: no distance sort (visit order only affects how fast U* shrinks, never the
               // result; modelled by tools/bvhsim, it costs ~1% more leaf tests and no node
               // visits).  Each write lands at the current top, which moves only for a push.
               node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : ch.x));
-              stk[sp * kBlock] = ch.x;
-              sp += (hk[0] && (hk[1] || hk[2] || hk[3])) ? 1u : 0u;
-              stk[sp * kBlock] = ch.y;
-              sp += (hk[1] && (hk[2] || hk[3])) ? 1u : 0u;
-              stk[sp * kBlock] = ch.z;
-              sp += (hk[2] && hk[3]) ? 1u : 0u;
-              if (sp > ka.stack_cap) {  // stack full: abandon, the exact linear scan decides
+              *top = ch.x;
+              top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlock : 0;
+              *top = ch.y;
+              top += (hk[1] && (hk[2] || hk[3])) ? kBlock : 0;
+              *top = ch.z;
+              top += (hk[2] && hk[3]) ? kBlock : 0;
+              if (top > stk_cap) {  // stack full: abandon, the exact linear scan decides
                 overflow = true;
-                sp = 0;
+                top = stk;
                 node = ykbvh::kEmptyLeaf;
               }
               continue;
@@ -678,9 +686,15 @@ void yk_render_persistent(KernelArgs ka) {
             }
             YK_STAMP(6);  // this leaf
           }
+#if YK_WIDE
+          if (top == stk) break;
+          top -= kBlock;
+          node = *top;
+#else
           if (sp == 0) break;
           --sp;
           node = stk[sp * kBlock];
+#endif
         }
         YK_STAMP(2);
         if (overflow) {
