@@ -5,22 +5,21 @@
 // samples → to_color3b) and the recursion of yk/raytracer.hpp:19-37.
 //
 // Execution model:
-//   * one PERSISTENT grid sized to the occupancy of the chip; every lane owns one PIXEL at a
-//     time and runs that pixel's samples in order s = 0, 1, ..., spp-1, adding each sample's
-//     colour to a per-lane float64 accumulator.  The reference's sum is strictly sequential
-//     (transform_reduce over an input-iterator iota; see oracle/yk_oracle.c pixel_sum), so
-//     keeping a pixel on one lane is what makes the sum bit-identical without storing samples.
-//   * the recursion is flattened into a loop of SEGMENTS (one closest-hit + scatter each).  A
-//     lane whose path ends starts its next sample on the next trip round the loop, and a lane
-//     whose pixel is done fetches the next pixel from a global counter (one wave-aggregated
-//     atomic per refill, __ballot/__popcll) — active-lane compaction by refill: no lane idles
-//     while the image has pixels left, however long its neighbours' bounce chains are.
-//   * the colour of a path is attenuation_1 * (attenuation_2 * (... * L)) — the reference
-//     multiplies back to front as the recursion unwinds, and double multiplication does not
-//     associate, so the lane keeps the ids of the scattering spheres on a small stack (8 in
-//     registers, the rest in a per-lane global spill) and multiplies back to front at the end.
-//   * sphere geometry is read wave-uniformly (scalar loads through the constant cache); the
-//     world tuple order is the array order, so the closest-hit scan is the reference's.
+//   * a render call is a few LAUNCHES of K samples per pixel (8, 32, 128, ... up to an 8 GB
+//     colour budget).  Per launch: yk_mt_warmup (x_397 of every sample's mt19937 seeding
+//     sequence, second stream), yk_render_persistent (the paths), yk_reduce_samples (the
+//     reference's strictly sequential per-pixel sum and to_color3b, third stream).
+//   * yk_render_persistent is one persistent grid over SAMPLE SLOTS: a lane runs one path at a
+//     time, one SEGMENT (closest hit + scatter) per trip round the loop, writes the sample's
+//     colour when the path ends and takes the next slot from a wave-level reserve (one atomic
+//     per 128 slots) — active-lane refill, so no lane idles while the launch has slots.
+//   * the colour of a path is attenuation_1 * (attenuation_2 * (... * L)): double
+//     multiplication does not associate, so the lane keeps the ids of the scattering spheres
+//     on a small stack (8 in registers, the rest in a per-lane global spill) and multiplies
+//     back to front at the end (raytracer.hpp:31).
+//   * closest hit: a 4-wide BVH in LDS culls conservatively in float, the candidates' roots
+//     are evaluated with the reference's exact arithmetic, ties to the later tuple index
+//      — the result equals the reference's ordered scan bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
