@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 4u
+#define YKGPU_ABI_VERSION 5u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 and DIELECTRIC are extensions needed by BASELINE configs 2-5 (no
@@ -119,14 +119,20 @@ typedef struct yk_render_params {
   uint32_t max_depth;         /* source.cpp:64                                          */
   uint32_t seed0;             /* constexpr_seed (source.cpp:118-120); 404 = "00:00:00"  */
   uint32_t row_begin;         /* rendered rows: row_begin + i*row_stride, i < row_count */
-  uint32_t row_count;         /*   (a tile of the image; the whole image: 0, H, 1)      */
-  uint32_t row_stride;
+  uint32_t row_count;         /*   (a tile of the image; the whole image: 0, H, 1), or   */
+  uint32_t row_stride;        /*   in bands of 2^row_band_log2 rows (below)             */
   uint32_t precision;         /* YK_PRECISION_*                                         */
   uint32_t rng;               /* YK_RNG_*                                               */
   uint32_t flags;             /* YK_FLAG_*                                              */
   uint32_t seed_mode;         /* YK_SEED_*                                              */
   double t_min;               /* 0.001 in the reference (raytracer.hpp:27)              */
   uint64_t seed_key;          /* YK_SEED_RANDOM_DEVICE only (0: draw one per call)      */
+  /* Banded row sets (the N-GPU split): with B = 2^row_band_log2, tile row i is image row
+   * row_begin + (i / B) * row_stride * B + i % B — bands of B consecutive rows, every
+   * row_stride-th band (rank k of N: row_begin = k*B, row_stride = N).  0: single rows.
+   * Whole bands keep a wave's pixels adjacent in the image (coherent rays); DESIGN.md §7. */
+  uint32_t row_band_log2;
+  uint32_t reserved0;
 } yk_render_params;
 
 typedef struct yk_render_stats {

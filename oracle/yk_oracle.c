@@ -215,12 +215,19 @@ typedef struct {
   int as_shipped;
 } job_t;
 
+/* Image row of tile row i of the row set (include/ykgpu.h: bands of 2^row_band_log2 rows, every
+ * row_stride-th band; 0 = single rows) */
+static uint64_t row_y(const yk_render_params* p, uint32_t i) {
+  const uint32_t L = p->row_band_log2;
+  return (uint64_t)p->row_begin + ((((uint64_t)(i >> L)) * p->row_stride) << L) + (i & ((1u << L) - 1u));
+}
+
 static void* worker(void* arg) {
   job_t* j = (job_t*)arg;
   world_t w = {j->s, j->n, j->cam, j->p, 0, j->as_shipped};
   const uint32_t W = j->p->image_width;
   for (uint32_t i = j->tid; i < j->p->row_count; i += j->nthreads) {
-    uint32_t y = j->p->row_begin + i * j->p->row_stride;
+    uint32_t y = row_y(j->p, i);
     for (uint32_t x = 0; x < W; ++x) {
       c3 ps = pixel_sum(&w, y, x, &j->segs);
       size_t o = ((size_t)i * W + x) * 3;
@@ -239,8 +246,8 @@ static void* worker(void* arg) {
 static int check(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p) {
   if (!s || !n || !cam || !p) return YK_ERR_INVALID;
   if (!p->image_width || !p->image_height || !p->samples_per_pixel) return YK_ERR_INVALID;
-  if (p->row_count && (p->row_stride == 0 ||
-      (uint64_t)p->row_begin + (uint64_t)(p->row_count - 1) * p->row_stride >= p->image_height))
+  if (p->row_count && (p->row_stride == 0 || p->row_band_log2 > 10 ||
+      row_y(p, p->row_count - 1) >= p->image_height))
     return YK_ERR_INVALID;
   if ((p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32) || (p->rng != YK_RNG_MT19937 && p->rng != YK_RNG_XOR128) ||
       p->seed_mode > YK_SEED_RANDOM_DEVICE || (p->seed_mode == YK_SEED_RANDOM_DEVICE && !p->seed_key))

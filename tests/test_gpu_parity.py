@@ -138,6 +138,35 @@ def test_row_tiles_reassemble(ren):
         np.testing.assert_array_equal(out, full)
 
 
+def test_banded_row_tiles_reassemble(ren):
+    """Bands of 2^k rows dealt cyclically (the N-GPU split of bench.py / tiles.py), including a
+    partial last band: the tiles reassemble into the reference golden image bit for bit."""
+    from uecraytracing_amd.tiles import tile_image_rows, tile_rows
+    e = next(c for c in MAN["cases"] if c["name"] == "mixed12_96x54x16_d50_s404")
+    ren.set_scene(refscenes.mixed12(), refscenes.reference_camera())
+    full = golden_data.rgb(e)
+    for n, L in ((2, 3), (3, 3), (8, 2), (4, 1), (3, 5)):
+        out = np.zeros_like(full)
+        for r in range(n):
+            rows = tile_rows(r, n, e["H"], L)
+            if rows[1] == 0:
+                continue
+            out[tile_image_rows(r, n, e["H"], L)] = ren.render(
+                make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], rows=rows))
+        np.testing.assert_array_equal(out, full)
+
+
+def test_banded_rows_of_the_headline_config(ren):
+    """Rank 5 of 8 at config 3 with bands of 8 rows (bench.py's split), first two bands vs the
+    oracle, sums bit for bit."""
+    arr, cam = yk.build_scene("final", 42)
+    ren.set_scene(arr, cam)
+    p = make_params(1920, 1080, 32, 50, 404, rows=(40, 16, 8, 3))  # rows 40-47 and 104-111
+    got = ren.render_sums(p)
+    _, want, _, _ = oracle_lib.render(arr, cam, p, nthreads=16, want_rgb=False, want_sums=True)
+    assert got.tobytes() == want.tobytes()
+
+
 def test_repeatable_and_counts(ren):
     arr, cam = yk.build_scene("final", 42)
     ren.set_scene(arr, cam)
@@ -221,6 +250,10 @@ def test_bad_rows_rejected(ren):
     ren.set_scene(refscenes.ref4(), refscenes.reference_camera())
     with pytest.raises(yk.YkError):
         ren.render(make_params(16, 9, 2, 50, 404, rows=(8, 2, 1)))
+    with pytest.raises(yk.YkError):  # banded: rows 0-3, then 8-11 (10, 11 outside)
+        ren.render(make_params(16, 9, 2, 50, 404, rows=(0, 8, 2, 2)))
+    with pytest.raises(yk.YkError):
+        ren.render(make_params(16, 9, 2, 50, 404, rows=(0, 1, 1, 11)))
 
 
 def _dupes_scene():

@@ -164,6 +164,25 @@ def test_row_tiles_concatenate_to_the_image():
         np.testing.assert_array_equal(out, full)
 
 
+def test_banded_row_tiles_concatenate_to_the_image():
+    """Bands of 2^k rows dealt cyclically (include/ykgpu.h row_band_log2) reassemble into the
+    reference golden image."""
+    from uecraytracing_amd.tiles import tile_image_rows, tile_rows
+    e = next(c for c in CASES if c["name"] == "ref4_33x17x5_d50_s7")
+    sph, cam = refscenes.ref4(), refscenes.reference_camera()
+    full = golden_data.rgb(e)
+    for n, L in ((2, 3), (3, 2), (4, 1)):
+        out = np.zeros_like(full)
+        for r in range(n):
+            rows = tile_rows(r, n, e["H"], L)
+            if rows[1] == 0:
+                continue
+            tile, _, _, _ = oracle_lib.render(sph, cam, make_params(e["W"], e["H"], e["spp"], e["depth"],
+                                                                   e["seed0"], rows=rows))
+            out[tile_image_rows(r, n, e["H"], L)] = tile
+        np.testing.assert_array_equal(out, full)
+
+
 def test_random_device_seed_hash():
     """YK_SEED_RANDOM_DEVICE's per-sample seed (include/ykgpu.h): splitmix64 of key + (idx+1)*phi,
     high word — restated here in Python against the oracle."""

@@ -1,6 +1,7 @@
-"""N>1 path on CPU: world_size-2 (and 3) gloo processes each render their cyclic row tile (the
-oracle stands in for the GPU here), gather to rank 0 through uecraytracing_amd.tiles — the same
-code bench.py runs over RCCL — and rank 0's image must equal the single-process image."""
+"""N>1 path on CPU: world_size-2 (and 3) gloo processes each render their row tile — bands of
+rows dealt cyclically, and single rows — (the oracle stands in for the GPU here), gather to rank 0
+through uecraytracing_amd.tiles — the same code bench.py runs over RCCL — and rank 0's image must
+equal the single-process image."""
 import os
 import socket
 import sys
@@ -18,7 +19,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, W, H, spp, out_path):
+def _worker(rank, world, port, W, H, spp, out_path, band_log2):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
     import torch
     import torch.distributed as dist
@@ -30,10 +31,10 @@ def _worker(rank, world, port, W, H, spp, out_path):
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    rows = tile_rows(rank, world, H)
+    rows = tile_rows(rank, world, H, band_log2)
     rgb, _, _, _ = oracle_lib.render(refscenes.mixed12(), refscenes.reference_camera(),
                                      make_params(W, H, spp, 50, 404, rows=rows), nthreads=2)
-    tg = TileGather(rank, world, H, W, "cpu")
+    tg = TileGather(rank, world, H, W, "cpu", band_log2)
     tg.tile[: rows[1]] = torch.from_numpy(rgb)
     img = tg.gather()
     if rank == 0:
@@ -42,25 +43,45 @@ def _worker(rank, world, port, W, H, spp, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_cyclic_tiles_gather_to_the_full_image(tmp_path, world):
+@pytest.mark.parametrize("world,band_log2", [(2, 3), (3, 3), (3, 1), (2, 0)])
+def test_cyclic_tiles_gather_to_the_full_image(tmp_path, world, band_log2):
     import oracle_lib
     import refscenes
     from uecraytracing_amd.records import make_params
     W, H, spp = 40, 23, 4
     out = str(tmp_path / "img.npy")
-    mp.spawn(_worker, args=(world, _free_port(), W, H, spp, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), W, H, spp, out, band_log2), nprocs=world, join=True)
     full, _, _, _ = oracle_lib.render(refscenes.mixed12(), refscenes.reference_camera(),
                                       make_params(W, H, spp, 50, 404))
     np.testing.assert_array_equal(np.load(out), full)
 
 
-def test_tile_rows_partition():
-    from uecraytracing_amd.tiles import assembly_index, rows_max, tile_rows
+def _row_y(rb, rs, L, t):
+    """include/ykgpu.h: tile row t of (row_begin, row_stride, row_band_log2)"""
+    return rb + (((t >> L) * rs) << L) + (t & ((1 << L) - 1))
+
+
+@pytest.mark.parametrize("band_log2", [0, 1, 3, 5])
+def test_tile_rows_partition(band_log2):
+    from uecraytracing_amd.tiles import assembly_index, rows_max, tile_image_rows, tile_rows
     for world in (1, 2, 3, 8):
-        for H in (1, 9, 112, 1080, 2160):
-            rows = [r for k in range(world) for r in range(*[tile_rows(k, world, H)[0], H, world])]
+        for H in (1, 9, 112, 450, 1080, 2160):
+            rows = []
+            for k in range(world):
+                rb, rc, rs, L = tile_rows(k, world, H, band_log2)
+                mine = [_row_y(rb, rs, L, t) for t in range(rc)]
+                assert mine == tile_image_rows(k, world, H, band_log2)
+                assert all(y < H for y in mine)
+                rows += mine
             assert sorted(rows) == list(range(H))
-            assert sum(tile_rows(k, world, H)[1] for k in range(world)) == H
-            idx = assembly_index(world, H).tolist()
-            assert len(set(idx)) == H and max(idx) < world * rows_max(world, H)
+            idx = assembly_index(world, H, band_log2=band_log2).tolist()
+            assert len(set(idx)) == H and max(idx) < world * rows_max(world, H, band_log2)
+
+
+def test_banded_tiles_are_balanced():
+    """Bands of 8 rows dealt cyclically: every rank of an 8-GPU split of 1080 rows gets 16 or
+    17 bands (max / mean rows <= 1.01)."""
+    from uecraytracing_amd.tiles import tile_rows
+    for world, H in ((2, 1080), (4, 1080), (8, 1080), (8, 2160)):
+        counts = [tile_rows(k, world, H)[1] for k in range(world)]
+        assert max(counts) / (H / world) <= 1.01, counts

@@ -119,7 +119,7 @@ constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 struct KernelArgs {
   yk_camera cam;
   uint32_t W, H, spp, max_depth;
-  uint32_t seed0, row_begin, row_count, row_stride;
+  uint32_t seed0, row_begin, row_count, row_stride, band_log2;
   uint32_t nspheres, pad_n, flags, id_stride;
   // A launch renders samples [s0, s0 + nsl / npix_slots) of every pixel: sample slot
   // i = s_local * npix_slots + p is sample s0 + s_local of tile pixel order[p].
@@ -145,6 +145,13 @@ struct KernelArgs {
   uint16_t* id_scratch;
   unsigned long long* counters;  // [segments, sphere_tests, sqrt_calls, mt_fallbacks, nodes]
 };
+
+// Image row of tile row t (include/ykgpu.h yk_render_params: bands of 2^band_log2 rows, every
+// row_stride-th band; band_log2 = 0 is the plain strided row set)
+__device__ __forceinline__ uint32_t tile_row_y(uint32_t row_begin, uint32_t row_stride, uint32_t band_log2,
+                                               uint32_t t) {
+  return row_begin + (((t >> band_log2) * row_stride) << band_log2) + (t & ((1u << band_log2) - 1u));
+}
 
 struct Hit {
   double T;
@@ -241,7 +248,7 @@ constexpr uint32_t kNoPixel = 0xffffffffu;
 // Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread,
 // one 16-B store.  out[i] = x_397(seed(i)), i = (pix - pix_base) * spp + s.
 struct WarmArgs {
-  uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode;
+  uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode, band_log2;
   uint64_t seed_key;
   const uint32_t* order;
   uint64_t n;  // sample slots in the launch
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       const uint32_t pix = q == kNoPixel ? 0u : q;
       const uint32_t sm = wa.s0 + sl;
       const uint32_t tr = pix / wa.W, xx = pix - tr * wa.W;
-      const uint32_t y = wa.row_begin + tr * wa.row_stride;
+      const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
       x[k] = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, sm);
     }
     ykd::mt_walk397x4(x);
@@ -461,7 +468,7 @@ void yk_render_persistent(KernelArgs ka) {
     if (start) {
       const uint32_t s = ka.s0 + slot / ka.npix_slots;
       const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
-      const uint32_t y = ka.row_begin + tr * ka.row_stride;
+      const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       // seed (uint32 wrap, source.cpp:154-158); mt19937's x_397 comes from yk_mt_warmup
       rng_start(g, ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka,
                 slot);
@@ -910,7 +917,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
     if (start) {
       const uint32_t s = ka.s0 + slot / ka.npix_slots;
       const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
-      const uint32_t y = ka.row_begin + tr * ka.row_stride;
+      const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       rng_start(g, ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka, slot);
       // (x + U01) / W with x, W unsigned → float (uniform_real_distribution<float>)
       const float u = ((float)x + f_uniform01(g)) / (float)ka.W;
@@ -1139,6 +1146,11 @@ struct ykgpu_context {
 
 namespace {
 
+uint64_t host_row_y(const yk_render_params* p, uint32_t t) {
+  const uint32_t L = p->row_band_log2;
+  return (uint64_t)p->row_begin + ((((uint64_t)(t >> L)) * p->row_stride) << L) + (t & ((1u << L) - 1u));
+}
+
 int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
   if (!ctx || !p) return fail(YK_ERR_INVALID, "null context or params");
   if (!ctx->have_scene) return fail(YK_ERR_NO_SCENE, "ykgpu_set_scene was not called");
@@ -1146,8 +1158,8 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
     return fail(YK_ERR_INVALID, "image_width, image_height and samples_per_pixel must be > 0");
   if (!p->row_count) return fail(YK_ERR_INVALID, "row_count must be > 0");
   if (!p->row_stride) return fail(YK_ERR_INVALID, "row_stride must be > 0");
-  if ((uint64_t)p->row_begin + (uint64_t)(p->row_count - 1) * p->row_stride >= p->image_height)
-    return fail(YK_ERR_INVALID, "row range outside the image");
+  if (p->row_band_log2 > 10) return fail(YK_ERR_INVALID, "row_band_log2 must be <= 10");
+  if (host_row_y(p, p->row_count - 1) >= p->image_height) return fail(YK_ERR_INVALID, "row range outside the image");
   if ((uint64_t)p->row_count * p->image_width >= (1ull << 31))
     return fail(YK_ERR_INVALID, "tile larger than 2^31 pixels");
   if (p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32)
@@ -1252,7 +1264,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       while (!seed_key) seed_key = ((uint64_t)rd() << 32) | rd();
     }
   }
-  rc = ensure_order(ctx, p->image_width, p->row_count, p->row_count > 1 ? p->row_stride : 1);
+  // image rows per tile row, for the shape of the processing blocks (bands of >= 8 rows: 1,
+  // an 8 x 8 block stays inside one band)
+  rc = ensure_order(ctx, p->image_width, p->row_count,
+                    p->row_count > 1 && p->row_band_log2 < 3 ? p->row_stride : 1);
   if (rc) return rc;
   // Launch schedule (samples per pixel per launch): 8, 32, 128, ... growing x4 up to the colour
   // budget (24 B per sample slot, kColourBytes per launch), the last one taking a small
@@ -1304,6 +1319,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.row_begin = p->row_begin;
   ka.row_count = p->row_count;
   ka.row_stride = p->row_stride;
+  ka.band_log2 = p->row_band_log2;
   ka.nspheres = ctx->nspheres;
   ka.flags = p->flags;
   ka.id_stride = ctx->id_stride;
@@ -1337,6 +1353,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.seed0 = p->seed0;
   wa.row_begin = p->row_begin;
   wa.row_stride = p->row_stride;
+  wa.band_log2 = p->row_band_log2;
   wa.out = ctx->d_warm;
   wa.npix_slots = nps;
   wa.seed_mode = p->seed_mode;

@@ -83,6 +83,8 @@ class RenderParams(ctypes.Structure):
         ("seed_mode", ctypes.c_uint32),
         ("t_min", ctypes.c_double),
         ("seed_key", ctypes.c_uint64),
+        ("row_band_log2", ctypes.c_uint32),  # bands of 2^k rows (include/ykgpu.h)
+        ("reserved0", ctypes.c_uint32),
     ]
 
 
@@ -119,7 +121,7 @@ class RenderStats(ctypes.Structure):
 
 assert ctypes.sizeof(Sphere) == 80
 assert ctypes.sizeof(Camera) == 19 * 8
-assert ctypes.sizeof(RenderParams) == 64
+assert ctypes.sizeof(RenderParams) == 72
 
 
 def image_height_for(width: int) -> int:
@@ -130,12 +132,12 @@ def image_height_for(width: int) -> int:
 def make_params(width, height=None, spp=8, max_depth=50, seed0=SEED0_EPOCH0, rows=None,
                 flags=0, t_min=T_MIN, precision=PRECISION_FP64, seed_mode=SEED_COUNTER,
                 seed_key=0, rng=RNG_MT19937) -> RenderParams:
-    """rows = (row_begin, row_count, row_stride); default: the whole image."""
+    """rows = (row_begin, row_count, row_stride[, row_band_log2]); default: the whole image."""
     if height is None:
         height = image_height_for(width)
-    rb, rc, rs = rows if rows is not None else (0, height, 1)
+    rb, rc, rs, band = (tuple(rows) + (0,))[:4] if rows is not None else (0, height, 1, 0)
     return RenderParams(width, height, spp, max_depth, seed0 & 0xFFFFFFFF, rb, rc, rs,
-                        precision, rng, flags, seed_mode, t_min, seed_key)
+                        precision, rng, flags, seed_mode, t_min, seed_key, band, 0)
 
 
 def sphere_array(spheres) -> ctypes.Array:
