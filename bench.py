@@ -224,7 +224,10 @@ def main():
             "launches_per_step": launches,
             "avg_launch_ms": round(launch_ms, 3),
             "note": "not HBM- or MFMA-bound: VALU issue and divergence (valu, pmc)",
-            "step_breakdown_ms": {"render": round(kernel_ms, 3), "mt_warmup": round(tst["warmup_ms"], 3),
+            # render = the launches' spans summed (consecutive launches overlap: launch c + 1
+            # takes the CUs launch c's draining blocks free); render_busy = their union
+            "step_breakdown_ms": {"render": round(kernel_ms, 3), "render_busy": round(tst["render_busy_ms"], 3),
+                                  "mt_warmup": round(tst["warmup_ms"], 3),
                                   "reduce": round(tst["resolve_ms"], 3), "call": round(call_ms, 3)},
             "valu": {
                 "achieved": round(achieved_tf, 3),

@@ -137,7 +137,8 @@ typedef struct yk_render_params {
 
 typedef struct yk_render_stats {
   double kernel_ms;        /* path-tracing kernel, summed over its launches (HIP events on
-                              the render stream around each launch)                     */
+                              the render stream around each launch; consecutive launches
+                              overlap, so this can exceed the call)                      */
   double resolve_ms;       /* ordered per-pixel sum + to_color3b kernel, summed           */
   double total_ms;         /* whole call: host wall clock for ykgpu_render / _sums (with
                               the copies), first to last event for ykgpu_render_async   */
@@ -161,6 +162,8 @@ typedef struct yk_render_stats {
   uint64_t seed_key;       /* the key a YK_SEED_RANDOM_DEVICE render used (0 otherwise) */
   uint32_t launches;       /* path-tracing launches in the call                        */
   uint32_t grid_blocks;    /* persistent grid size                                     */
+  double render_busy_ms;   /* union of the path-tracing launches' spans (wall time with at
+                              least one launch running)                                 */
 } yk_render_stats;
 
 typedef struct ykgpu_context ykgpu_context;

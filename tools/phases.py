@@ -8,7 +8,8 @@ spp = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 arr, cam = yk.build_scene(scene, 42)
 with yk.Renderer(0) as r:
     r.set_scene(arr, cam)
-    p = make_params(1920, None, spp, 50, 404, flags=1)
+    rows = tuple(int(v) for v in os.environ["ROWS"].split(":")) if os.environ.get("ROWS") else None
+    p = make_params(1920, None, spp, 50, 404, rows=rows, flags=1)
     r.render(p); r.render(p)
     st = r.stats()
     pc = st["phase_cycles"]
@@ -22,7 +23,7 @@ with yk.Renderer(0) as r:
         print(f"timeline: pixels exhausted at {(tl[1] - tl[0]) / span * 100:.1f}% of the launch "
               f"({span / 1e5:.1f} ms), tail {(tl[2] - tl[1]) / span * 100:.1f}%")
     diag = st["diag"]
-    r.render(make_params(1920, None, spp, 50, 404, flags=1))
+    r.render(make_params(1920, None, spp, 50, 404, rows=rows, flags=1))
     st2 = r.stats()
     print(f"leaf tests {st2['sphere_tests']}, with disc >= 0 {diag[0]} ({diag[0] / max(1, st2['sphere_tests']):.3f})")
     print(f"node visits (lanes) {st2['node_visits']}, wave-level node-loop iterations {node_iters} -> "

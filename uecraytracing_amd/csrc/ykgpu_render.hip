@@ -1113,6 +1113,7 @@ struct ykgpu_context {
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;  // the MT warm-ups run here, beside the render launches
   hipStream_t red = nullptr;  // the ordered reduces run here, beside the next render launch
+  hipStream_t alt = nullptr;  // odd render launches: a launch starts while the previous drains
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> lev;  // per launch: warm-up start, render start, reduce start, end
   uint32_t lev_used = 0;
@@ -1178,7 +1179,7 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, int grid, bool need_m
     (void)hipFree(ctx->d_mt);
     ctx->d_mt = nullptr;
     ctx->scratch_lanes = 0;
-    YK_HIP(hipMalloc(&ctx->d_mt, lanes * ykd::kMtN * sizeof(uint32_t)));
+    YK_HIP(hipMalloc(&ctx->d_mt, 2 * lanes * ykd::kMtN * sizeof(uint32_t)));  // two launches in flight
     ctx->scratch_lanes = lanes;
   }
   // attenuation-id spill: max_depth u16 per lane
@@ -1188,7 +1189,7 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, int grid, bool need_m
     ctx->d_ids = nullptr;
     ctx->id_stride = 0;
     ctx->id_lanes = 0;
-    YK_HIP(hipMalloc(&ctx->d_ids, lanes * need * sizeof(uint16_t)));
+    YK_HIP(hipMalloc(&ctx->d_ids, 2 * lanes * need * sizeof(uint16_t)));
     ctx->id_stride = need;
     ctx->id_lanes = lanes;
   }
@@ -1344,8 +1345,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.seed_mode = p->seed_mode;
   ka.seed_key = seed_key;
   ka.pixel_counter = ctx->d_counter;
-  ka.mt_scratch = ctx->d_mt;
-  ka.id_scratch = ctx->d_ids;
+
   ka.counters = ctx->d_stats;
   WarmArgs wa;
   wa.W = p->image_width;
@@ -1392,6 +1392,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   }
   ctx->lev_used = 6 * nlaunch;
   YK_HIP(hipStreamWaitEvent(ctx->red, ctx->ev0, 0));
+  YK_HIP(hipStreamWaitEvent(ctx->alt, ctx->ev0, 0));
   auto warm = [&](uint32_t c) -> int {
     hipEvent_t* ev = &ctx->lev[6 * c];
     if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
@@ -1419,19 +1420,26 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.nsl = nsl;
     ka.col = col;
     ka.warm = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
-    YK_HIP(hipStreamWaitEvent(st, ev[1], 0));                                // its x_397
-    if (c >= 2) YK_HIP(hipStreamWaitEvent(st, ctx->lev[6 * (c - 2) + 5], 0));  // its colour buffer
+    // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
+    // only on its own x_397 and colour buffer, so its blocks take the CUs that launch c's
+    // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
+    const hipStream_t rs = (c & 1) ? ctx->alt : st;
+    const size_t lanes = (size_t)grid * kBlock;
+    ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (c & 1) * lanes * ykd::kMtN : nullptr;
+    ka.id_scratch = ctx->d_ids + (c & 1) * lanes * ctx->id_stride;
+    YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its x_397
+    if (c >= 2) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - 2) + 5], 0));  // its colour buffer
     ka.pixel_counter = ctx->d_counter + c;
-    YK_HIP(hipEventRecord(ev[2], st));
+    YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (f32)
-      hipLaunchKernelGGL(f32_kernel((count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(kBlock), 0, st, ka);
+      hipLaunchKernelGGL(f32_kernel((count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(kBlock), 0, rs, ka);
     else
       hipLaunchKernelGGL(fp64_kernel(ctx->scene_in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
                                                             (x128 ? 4 : 0)),
-                         dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, st, ka);
+                         dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, rs, ka);
     YK_HIP(hipGetLastError());
-    YK_HIP(hipEventRecord(ev[3], st));
+    YK_HIP(hipEventRecord(ev[3], rs));
     ra.col = col;
     ra.nsl = nsl;
     ra.ks = ks;
@@ -1471,7 +1479,7 @@ int finish_stats(ykgpu_context* ctx) {
   for (int k = 0; k < 3; ++k) ctx->stats.timeline[k] = c[16 + k];
   for (int k = 0; k < 4; ++k) ctx->stats.diag[k] = c[19 + k];
   ctx->stats.total_ms = ms;
-  double tw = 0, tr = 0, tp = 0;
+  double tw = 0, tr = 0, tp = 0, busy = 0;
   for (uint32_t k = 0; k + 5 < ctx->lev_used; k += 6) {
     float a = 0, b = 0, c = 0;
     YK_HIP(hipEventSynchronize(ctx->lev[k + 5]));
@@ -1479,7 +1487,12 @@ int finish_stats(ykgpu_context* ctx) {
     YK_HIP(hipEventElapsedTime(&b, ctx->lev[k + 2], ctx->lev[k + 3]));
     YK_HIP(hipEventElapsedTime(&c, ctx->lev[k + 4], ctx->lev[k + 5]));
     tw += a, tr += b, tp += c;
+    // union of the render spans: launch k/6 overlaps only the tail of the one before it
+    float ov = 0;
+    if (k >= 6) YK_HIP(hipEventElapsedTime(&ov, ctx->lev[k + 2], ctx->lev[k - 6 + 3]));
+    busy += b - std::min<double>(b, std::max<double>(0.0, ov));
   }
+  ctx->stats.render_busy_ms = busy;
   ctx->stats.warmup_ms = tw;
   ctx->stats.kernel_ms = tr;
   ctx->stats.resolve_ms = tp;
@@ -1532,6 +1545,7 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->alt, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
     ykgpu_context_destroy(ctx);
@@ -1567,6 +1581,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->red) (void)hipStreamDestroy(ctx->red);
+  if (ctx->alt) (void)hipStreamDestroy(ctx->alt);
   delete ctx;
   return YK_OK;
 }

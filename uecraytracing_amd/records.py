@@ -109,6 +109,7 @@ class RenderStats(ctypes.Structure):
         ("seed_key", ctypes.c_uint64),
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
+        ("render_busy_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
