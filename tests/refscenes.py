@@ -61,3 +61,26 @@ def walls2():
 
 
 SCENES = {"ref4": ref4, "lambert3": lambert3, "mixed12": mixed12, "walls2": walls2}
+
+
+def dupes():
+    """Six exactly coincident spheres (ties: the last tuple index must win) plus a ground and a
+    far sphere: candidate-list overflow and origins beyond the trees' bound."""
+    s = [lambertian((0, -100.5, -1), 100.0, (0.8, 0.8, 0.0))]
+    for k in range(6):
+        s.append((lambertian if k % 2 else metal)((0, 0, -1), 0.5, (0.1 * k + 0.3, 0.5, 0.9 - 0.1 * k)))
+    s.append(lambertian((3000.0, 0.0, -1.0), 2900.0, (0.2, 0.3, 0.4)))
+    return s
+
+
+def graze():
+    """Near-tangent rays for the float culling bound: the camera's horizon skims a ground sphere
+    1e-4 below it, a mirror 800 units away shows its silhouette, the upper rows graze a ceiling
+    sphere, and two small spheres sit on the ground."""
+    return [
+        lambertian((0, -1000.0, -1), 999.9999, (0.5, 0.5, 0.5)),
+        metal((0, 0, -800), 100.0, (0.9, 0.9, 0.9)),
+        lambertian((0, 300.3, -1), 300.0, (0.8, 0.9, 0.95)),
+        metal((0.4, -0.1, -1.5), 0.1, (0.9, 0.8, 0.7)),
+        lambertian((-0.4, -0.0999, -1.2), 0.1, (0.2, 0.8, 0.3)),
+    ]

@@ -14,7 +14,8 @@ with yk.Renderer(0) as r:
     r.set_scene(arr, cam)
     for name, kw, s in [("mt19937/fp64", {}, spp), ("xor128/fp64", {"rng": RNG_XOR128}, spp),
                         ("mt19937/fp32", {"precision": PRECISION_FP32}, spp32),
-                        ("xor128/fp32", {"precision": PRECISION_FP32, "rng": RNG_XOR128}, spp32)]:
+                        ("xor128/fp32", {"precision": PRECISION_FP32, "rng": RNG_XOR128}, spp32),
+                        ("mt19937/fp32 linear scan", {"precision": PRECISION_FP32, "flags": 2}, 16)]:
         p = make_params(1920, None, s, 50, 404, **kw)
         r.render(p)
         ts = []

@@ -141,7 +141,7 @@ Built build(const double* centers, const double* radii, uint32_t n, double camer
     bd.idx.resize(n);
     std::iota(bd.idx.begin(), bd.idx.end(), 0u);
     for (uint32_t i = 0; i < n; ++i) {
-      const double r = std::fabs(radii[i]) + out.delta;
+      const double r = std::fabs(radii[i]) * (1.0 + opt.radius_grow) + out.delta;
       for (int k = 0; k < 3; ++k) {
         bd.sbox[i].lo[k] = centers[3 * i + k] - r;
         bd.sbox[i].hi[k] = centers[3 * i + k] + r;

@@ -55,6 +55,13 @@ struct alignas(16) WideNode {
 static_assert(sizeof(WideNode) == 160, "WideNode layout");
 constexpr int32_t kEmptyLeaf = ~0;  // leaf code with no spheres
 
+// render<float>'s sphere test (sphere.hpp:25-48 evaluated in float) near tangency: a root it
+// accepts puts the exact point o + r d within 2^-8.9 (|o - c| + |radius|) of the float sphere,
+// hence within 2^-8.9 (r |d| + 2 |radius|).  FP32 trees grow each sphere's box
+// by 2 kF32Cone |radius| on top of delta, and the FP32 kernel widens every ray into a cone of
+// slope kF32Cone |d|: 1.87x the bound.
+constexpr float kF32Cone = 0x1p-8f * (1.0f + 0x1p-10f);
+
 struct Built {
   std::vector<Node> nodes;      // nodes[0] is the root when root >= 0
   std::vector<uint32_t> order;  // leaf slots → original sphere index (tuple order)
@@ -67,6 +74,7 @@ struct Built {
 struct Options {
   uint32_t max_leaf = 2;  // spheres per leaf (<= 15); 2 measured best on the final scene
   int bins = 16;          // SAH bins per split
+  double radius_grow = 0; // extra box growth per unit |radius| (FP32 trees: 2 kF32Cone)
 };
 
 // centers: 3 doubles per sphere; radii may be negative (hollow shells: |r| is used).

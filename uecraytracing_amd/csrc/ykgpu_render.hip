@@ -879,23 +879,85 @@ RenderKernel fp64_kernel(bool lds, int mode) {
 // ---- render<float> (YK_PRECISION_FP32) ---------------------------------------------------
 // The same persistent, sample-parallel structure as yk_render_persistent (refill, slots, MT
 // cursors from yk_mt_warmup, attenuation-id stack, SoA colours reduced by yk_reduce_samples),
-// with the path in float (yk_device_f32.hpp).  Closest hit is the reference's linear scan
-// (hittable_list.hpp:32-58) over float geometry read wave-uniformly (scalar loads): the BVH's
-// culling proof bounds FP64 rounding, not FP32's.
+// with the path in float (yk_device_f32.hpp).  Closest hit: the FP32 tree culls — its boxes and
+// a per-ray cone carry the float sphere test's proven error — and every sphere
+// of an entered leaf gets the reference's float test itself (as cheap as bounds would be, so
+// there is no candidate stage): the minimum root wins, an exact tie goes to the later tuple
+// index.  Rays outside the tree's proven range take the ordered scan (hittable_list.hpp:32-58).
 template <class G>
 __device__ __forceinline__ float f_uniform01(G& g) { return ykf::uniform(g, 0.0f, 1.0f); }
 
-// kMode bit 0: the work counters; bit 2: the yk::xor128 engine (as for the FP64 kernel)
-template <int kMode>
+// sphere::hit_impl<float> (sphere.hpp:25-48) bit for bit, without t_max.  Returns 2 with the root
+// in r (root1 if >= tmin, else root2: the reference accepts it iff r <= t_max, because root2 >=
+// root1 under monotonic rounding), 1 when both roots lie below tmin, 0 when disc < 0.
+__device__ __forceinline__ int f32_root(float4 sg, ykf::v3 o, ykf::v3 d, float a, float tmin, float& r,
+                                        uint32_t& nit) {
+  const ykf::v3 oc = {o.x - sg.x, o.y - sg.y, o.z - sg.z};
+  const float hb = ykf::dot(oc, d);
+  const float c = ykf::len2(oc) - sg.w;
+  const float disc = hb * hb - a * c;
+  if (disc < 0) return 0;
+  const float sq = ykf::nsqrt(disc, nit);
+  r = (-hb - sq) / a;
+  if (r < tmin) {
+    r = (-hb + sq) / a;
+    if (r < tmin) return 1;
+  }
+  return 2;
+}
+
+// One axis of the ray's cone: near planes are crossed at (plane - o) * in, far
+// planes at (plane - o) * jf, with in = 1/(d + s sign d) and jf = (1 + 2^-17)/(d - s sign d); an
+// axis with |d| < 2s keeps no far bound (jf = 0, constant +inf).  Slab FMA operands: plane * in +
+// nc.  Culling arithmetic only: v_rcp_f32's ulp is inside the relative margins.
+__device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, f2& nc2, f2& jf2, f2& fc2) {
+  const float sg = dk < 0.0f ? -s : s;
+  const float in = __builtin_amdgcn_rcpf(dk + sg);
+  const bool far = fabsf(dk) >= 2.0f * s;
+  const float jf = far ? __builtin_amdgcn_rcpf(dk - sg) * (1.0f + 0x1p-17f) : 0.0f;
+  const float nc = -(ok * in), fc = far ? -(ok * jf) : INFINITY;
+  in2 = f2{in, in};
+  nc2 = f2{nc, nc};
+  jf2 = f2{jf, jf};
+  fc2 = f2{fc, fc};
+}
+
+// kSceneInLds: the FP32 tree, its float4 leaf geometry and its leaf ids copied into LDS per
+// workgroup, as in the FP64 kernel.  kMode bit 0: the work counters; bit 2: the yk::xor128
+// engine (as for the FP64 kernel)
+template <bool kSceneInLds, int kMode>
 __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
   constexpr bool kCount = (kMode & 1) != 0;
   using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const char* __restrict__ nodes = (const char*)ka.nodes;
+  const float4* __restrict__ leaf_geo = (const float4*)ka.leaf_geo;
+  const uint32_t* __restrict__ leaf_ids = ka.leaf_ids;
+  if (kSceneInLds) {
+    const uint4* src[3] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids};
+    const uint32_t off[3] = {0u, ka.lds_geo_off, ka.lds_ids_off};
+    const uint32_t n16[3] = {(ka.n_nodes * (uint32_t)sizeof(DevNode) + 15u) / 16u, ka.nspheres,
+                             (ka.nspheres + 3u) / 4u};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      uint4* dst = (uint4*)(smem + off[k]);
+      for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlock) dst[i] = src[k][i];
+    }
+    __syncthreads();
+    nodes = smem;
+    leaf_geo = (const float4*)(smem + ka.lds_geo_off);
+    leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
+  }
+  int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlock]
+#if YK_RENDER_PRIO
+  __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);  // over the co-resident warm-up waves, as in FP64
+#endif
   Gen g;
   rng_init(g, ka, gid);
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
-  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_nit = 0, n_ncall = 0;
+  uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_nit = 0, n_ncall = 0, n_node = 0, n_lin = 0;
   const float tmin = (float)ka.t_min;  // world.hit(r, 0.001, ...) converts to T (hittable.hpp:32)
   uint32_t slot = 0, depth = 0, nstk = 0;
   uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
@@ -943,30 +1005,118 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
       in_path = true;
     }
 
-    // ---- closest hit: the reference's ordered scan in float (sphere.hpp:25-48)
+    // ---- closest hit (hittable_list.hpp:32-58 over sphere.hpp:25-48, in float)
     const bool alive = in_path && depth != 0;
     float T = INFINITY;
     int hid = -1;
     if (alive) {
       ++n_seg;
       const float a = ykf::len2(d);
-      for (uint32_t i = 0; i < ka.nspheres; ++i) {
-        const float4 sg = ka.geo_f[i];  // wave-uniform: scalar loads
-        if (kCount) ++n_test;
-        const ykf::v3 oc = {o.x - sg.x, o.y - sg.y, o.z - sg.z};
-        const float hb = ykf::dot(oc, d);
-        const float c = ykf::len2(oc) - sg.w;
-        const float disc = hb * hb - a * c;
-        if (disc < 0) continue;
-        if (kCount) ++n_sqrt, ++n_ncall;
-        const float sq = ykf::nsqrt(disc, n_nit);
-        float root = (-hb - sq) / a;
-        if (root < tmin || T < root) {
-          root = (-hb + sq) / a;
-          if (root < tmin || T < root) continue;
+      const float onorm = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+      // the tree serves the rays its bound is proven for: |d|^2 in [2^-60, 2^60],
+      // origin within origin_bound (< 0: the scene is outside the proven scale); the rest scan
+      bool linear = (ka.flags & kFlagLinearScan) || !YK_WIDE || !(a >= 0x1p-60f && a <= 0x1p60f) ||
+                    !((double)onorm <= ka.origin_bound);
+#if YK_WIDE
+      if (!linear) {
+        f2 inx, ncx, jfx, fcx, iny, ncy, jfy, fcy, inz, ncz, jfz, fcz;
+        const float s = __builtin_sqrtf(a) * ykbvh::kF32Cone;  // the cone's slope (>= kF32Cone |d|)
+        cone_axis(d.x, o.x, s, inx, ncx, jfx, fcx);
+        cone_axis(d.y, o.y, s, iny, ncy, jfy, fcy);
+        cone_axis(d.z, o.z, s, inz, ncz, jfz, fcz);
+        // the (near x4, far x4) plane quads of the ray's direction signs inside a WideNode
+        const char* const px = nodes + (d.x < 0.0f ? 16u : 0u);
+        const char* const py = nodes + 48u + (d.y < 0.0f ? 16u : 0u);
+        const char* const pz = nodes + 96u + (d.z < 0.0f ? 16u : 0u);
+        const float tmin_lo = tmin * (1.0f - 0x1p-17f);
+        float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
+        uint32_t overflow = 0;  // (a VGPR, not a lane-mask bool, across the loop's divergent exits)
+        int32_t node = ka.bvh_root;
+        int32_t* top = stk;
+        const int32_t* const stk_cap = stk + ka.stack_cap * kBlock;
+        for (;;) {
+          if (node >= 0) {
+            if (kCount) ++n_node;
+            // the FP64 kernel's visit (same planes, margins and visit order), the cone's operands
+            const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
+            const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
+            const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
+            const int4 ch = *(const int4*)(nodes + node + 144);
+            const f2 nx[2] = {__builtin_elementwise_fma(qnx.xy, inx, ncx), __builtin_elementwise_fma(qnx.zw, inx, ncx)};
+            const f2 fx[2] = {__builtin_elementwise_fma(qfx.xy, jfx, fcx), __builtin_elementwise_fma(qfx.zw, jfx, fcx)};
+            const f2 ny[2] = {__builtin_elementwise_fma(qny.xy, iny, ncy), __builtin_elementwise_fma(qny.zw, iny, ncy)};
+            const f2 fy[2] = {__builtin_elementwise_fma(qfy.xy, jfy, fcy), __builtin_elementwise_fma(qfy.zw, jfy, fcy)};
+            const f2 nz[2] = {__builtin_elementwise_fma(qnz.xy, inz, ncz), __builtin_elementwise_fma(qnz.zw, inz, ncz)};
+            const f2 fz[2] = {__builtin_elementwise_fma(qfz.xy, jfz, fcz), __builtin_elementwise_fma(qfz.zw, jfz, fcz)};
+            bool hk[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float tn = fmaxf(fmaxf(fmaxf(nx[k >> 1][k & 1], ny[k >> 1][k & 1]), nz[k >> 1][k & 1]), tmin_lo);
+              const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
+              hk[k] = tn <= tf;
+            }
+            asm volatile("" ::"v"(ch.x), "v"(ch.y), "v"(ch.z), "v"(ch.w));
+            if (hk[0] || hk[1] || hk[2] || hk[3]) {
+              node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : ch.x));
+              *top = ch.x;
+              top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlock : 0;
+              *top = ch.y;
+              top += (hk[1] && (hk[2] || hk[3])) ? kBlock : 0;
+              *top = ch.z;
+              top += (hk[2] && hk[3]) ? kBlock : 0;
+              if (top > stk_cap) {  // stack full: abandon, the linear scan decides
+                overflow = 1;
+                top = stk;
+                node = ykbvh::kEmptyLeaf;
+              }
+              continue;
+            }
+          } else {
+            const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
+            for (uint32_t k = 0; k < cnt; ++k) {
+              if (kCount) ++n_test;
+              float r = 0.0f;
+              const int res = f32_root(leaf_geo[first + k], o, d, a, tmin, r, n_nit);
+              if (kCount && res > 0) ++n_sqrt, ++n_ncall;
+              if (res < 2) continue;
+              // closest wins, an exact tie goes to the later tuple index (hittable_list.hpp:36-43)
+              const int id = (int)leaf_ids[first + k];
+              if (r < T || (r == T && id > hid)) {
+                T = r;
+                hid = id;
+                ustar_f = r * (1.0f + 0x1p-18f);
+              }
+            }
+          }
+          if (top == stk) break;
+          top -= kBlock;
+          node = *top;
         }
-        T = root;
-        hid = (int)i;
+        if (overflow != 0) linear = true;
+      }
+#endif
+      if (linear) {  // the reference's ordered scan in tuple order (wave-uniform scalar loads)
+        ++n_lin;
+        T = INFINITY;
+        hid = -1;
+        for (uint32_t i = 0; i < ka.nspheres; ++i) {
+          const float4 sg = ka.geo_f[i];
+          if (kCount) ++n_test;
+          const ykf::v3 oc = {o.x - sg.x, o.y - sg.y, o.z - sg.z};
+          const float hb = ykf::dot(oc, d);
+          const float c = ykf::len2(oc) - sg.w;
+          const float disc = hb * hb - a * c;
+          if (disc < 0) continue;
+          if (kCount) ++n_sqrt, ++n_ncall;
+          const float sq = ykf::nsqrt(disc, n_nit);
+          float root = (-hb - sq) / a;
+          if (root < tmin || T < root) {
+            root = (-hb + sq) / a;
+            if (root < tmin || T < root) continue;
+          }
+          T = root;
+          hid = (int)i;
+        }
       }
     }
 
@@ -1070,16 +1220,20 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
     atomicAdd(&ka.counters[1], (unsigned long long)n_test);
     atomicAdd(&ka.counters[2], (unsigned long long)n_sqrt);
-    atomicAdd(&ka.counters[5], (unsigned long long)n_seg);  // every segment is a linear scan
+    atomicAdd(&ka.counters[4], (unsigned long long)n_node);
+    atomicAdd(&ka.counters[5], (unsigned long long)n_lin);
     atomicAdd(&ka.counters[6], (unsigned long long)n_ncall);
     atomicAdd(&ka.counters[7], (unsigned long long)n_nit);
   }
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
 
-RenderKernel f32_kernel(int mode) {
-  static const RenderKernel k[4] = {yk_render_f32<0>, yk_render_f32<1>, yk_render_f32<4>, yk_render_f32<5>};
-  return k[(mode & 1) | ((mode & 4) >> 1)];
+// The FP32 instance for (scene in LDS, kMode)
+RenderKernel f32_kernel(bool lds, int mode) {
+  static const RenderKernel k[8] = {yk_render_f32<false, 0>, yk_render_f32<false, 1>, yk_render_f32<false, 4>,
+                                    yk_render_f32<false, 5>, yk_render_f32<true, 0>,  yk_render_f32<true, 1>,
+                                    yk_render_f32<true, 4>,  yk_render_f32<true, 5>};
+  return k[(lds ? 4 : 0) + ((mode & 1) | ((mode & 4) >> 1))];
 }
 
 // ykgpu_math_sqrt_f32: the FP32 path's math::sqrt<float> on a buffer (diagnostic).
@@ -1094,15 +1248,34 @@ __global__ __launch_bounds__(256) void yk_math_sqrt_f32(const float* in, float* 
 // =========================================================================================
 // C-ABI
 // =========================================================================================
+// A BVH on the device: the FP64 kernel's (boxes grown for the exact test's rounding, DESIGN.md
+// §4) or the FP32 kernel's (grown for render<float>'s sphere test, §4.1), with its LDS layout
+// [nodes][leaf geometry][leaf ids][traversal stacks] and the persistent grid it leaves room for.
+struct DevTree {
+  DevNode* nodes = nullptr;
+  void* leaf_geo = nullptr;      // SphereGeo (FP64) or float4 (FP32), in leaf order
+  uint32_t* leaf_ids = nullptr;  // leaf slot → tuple index
+  int32_t root = 0;              // root code (byte offset of the root node, or a leaf code)
+  uint32_t depth = 0, n_nodes = 0;
+  double origin_bound = 0;  // |o|_inf beyond which a ray takes the linear scan (< 0: every ray)
+  bool in_lds = false;
+  uint32_t lds_bytes = 0, geo_off = 0, ids_off = 0, stack_off = 0, stack_cap = 0, stack_entries = 0;
+  int grid = 0;  // persistent blocks: occupancy x CUs
+  void release() {
+    (void)hipFree(nodes);
+    (void)hipFree(leaf_geo);
+    (void)hipFree(leaf_ids);
+    nodes = nullptr;
+    leaf_geo = nullptr;
+    leaf_ids = nullptr;
+  }
+};
+
 struct ykgpu_context {
   int device = 0;
   int cus = 0;
-  int grid = 0;      // persistent blocks for the current scene (FP64 kernel)
-  int grid_f32 = 0;  // persistent blocks of the FP32 kernel
+  DevTree t64, t32;  // the FP64 and FP32 kernels' trees over the current scene
   size_t scratch_lanes = 0;
-  bool scene_in_lds = false;
-  uint32_t lds_bytes = 0, lds_geo_off = 0, lds_ids_off = 0, lds_stack_off = 0, stack_entries = 0, stack_cap = 0;
-  uint32_t n_nodes = 0;
   uint32_t* d_warm = nullptr;  // x_397 per sample slot of one launch
   double* d_col = nullptr;     // sample colours of one launch (SoA)
   double* d_acc = nullptr;     // running per-pixel sums between launches
@@ -1126,13 +1299,7 @@ struct ykgpu_context {
   uint32_t* d_counter = nullptr;        // sample-slot counters, one per launch of a call
   uint32_t counter_cap = 0;
   unsigned long long* d_stats = nullptr;  // kCounters counters
-  DevNode* d_nodes = nullptr;
-  SphereGeo* d_leaf_geo = nullptr;
-  uint32_t* d_leaf_ids = nullptr;
-  int32_t bvh_root = 0;
-  uint32_t bvh_depth = 0;
-  double origin_bound = 0;
-  uint32_t* d_mt = nullptr;             // grid*256*624 words
+  uint32_t* d_mt = nullptr;            // grid*256*624 words
   uint16_t* d_ids = nullptr;            // grid*256*id_stride
   uint32_t id_stride = 0;
   size_t id_lanes = 0;
@@ -1253,7 +1420,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
            hipStream_t st) {
   const bool f32 = p->precision == YK_PRECISION_FP32;
   const bool x128 = p->rng == YK_RNG_XOR128;  // no x_397 warm-ups, no MT scratch
-  const int grid = f32 ? ctx->grid_f32 : ctx->grid;
+  const DevTree& tree = f32 ? ctx->t32 : ctx->t64;
+  const int grid = tree.grid;
   int rc = ensure_scratch(ctx, p->max_depth, grid, !x128);
   if (rc) return rc;
   // YK_SEED_RANDOM_DEVICE without a key: one from std::random_device per call (source.cpp:159)
@@ -1327,18 +1495,18 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.warm = ctx->d_warm;
   ka.order = ctx->d_order;
   ka.t_min = p->t_min;
-  ka.origin_bound = ctx->origin_bound;
+  ka.origin_bound = tree.origin_bound;
   ka.inv_w = 1.0 / (double)ka.W;
   ka.inv_h = 1.0 / (double)ka.H;
-  ka.bvh_root = ctx->bvh_root;
-  ka.n_nodes = ctx->n_nodes;
-  ka.lds_geo_off = ctx->lds_geo_off;
-  ka.lds_ids_off = ctx->lds_ids_off;
-  ka.lds_stack_off = ctx->lds_stack_off;
-  ka.stack_cap = ctx->stack_cap;
-  ka.nodes = ctx->d_nodes;
-  ka.leaf_geo = ctx->d_leaf_geo;
-  ka.leaf_ids = ctx->d_leaf_ids;
+  ka.bvh_root = tree.root;
+  ka.n_nodes = tree.n_nodes;
+  ka.lds_geo_off = tree.geo_off;
+  ka.lds_ids_off = tree.ids_off;
+  ka.lds_stack_off = tree.stack_off;
+  ka.stack_cap = tree.stack_cap;
+  ka.nodes = tree.nodes;
+  ka.leaf_geo = (const SphereGeo*)tree.leaf_geo;  // float4 records for the FP32 kernel
+  ka.leaf_ids = tree.leaf_ids;
   ka.geo = ctx->d_geo;
   ka.mat = ctx->d_mat;
   ka.geo_f = ctx->d_geo_f;
@@ -1433,11 +1601,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (f32)
-      hipLaunchKernelGGL(f32_kernel((count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(kBlock), 0, rs, ka);
+      hipLaunchKernelGGL(f32_kernel(tree.in_lds, (count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(kBlock),
+                         tree.lds_bytes, rs, ka);
     else
-      hipLaunchKernelGGL(fp64_kernel(ctx->scene_in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
-                                                            (x128 ? 4 : 0)),
-                         dim3(ctx->grid), dim3(kBlock), ctx->lds_bytes, rs, ka);
+      hipLaunchKernelGGL(fp64_kernel(tree.in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
+                                                      (x128 ? 4 : 0)),
+                         dim3(grid), dim3(kBlock), tree.lds_bytes, rs, ka);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[3], rs));
     ra.col = col;
@@ -1504,6 +1673,73 @@ int finish_stats(ykgpu_context* ctx) {
   return YK_OK;
 }
 
+// Builds one BVH over the scene and uploads it into t: `geo` holds the tuple-order geometry the
+// kernel's leaves read (`elem` bytes per sphere), stored in leaf order; kern_lds / kern_glob are
+// the kernel instances that read the tree from LDS / global memory (for the occupancy).
+int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
+                double cam_ext, const ykbvh::Options& opt, const void* geo, size_t elem, RenderKernel kern_lds,
+                RenderKernel kern_glob) {
+  const uint32_t count = (uint32_t)radii.size();
+  const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
+  if (bvh.depth > ykbvh::kMaxDepth) return fail(YK_ERR_INVALID, "BVH deeper than the traversal stack");
+  std::vector<char> leaf_geo(count * elem);
+  for (uint32_t i = 0; i < count; ++i)
+    std::memcpy(leaf_geo.data() + i * elem, (const char*)geo + (size_t)bvh.order[i] * elem, elem);
+  t.release();
+#if YK_WIDE
+  int32_t root_code = 0;
+  uint32_t wdepth = 0;
+  const std::vector<DevNode> snodes = ykbvh::wide_nodes(bvh, &root_code, &wdepth);
+#else
+  const std::vector<DevNode> snodes = ykbvh::slab_nodes(bvh);
+  const int32_t root_code = ykbvh::slab_root(bvh);
+#endif
+  const size_t nn = std::max<size_t>(1, snodes.size());
+  YK_HIP(hipMalloc(&t.nodes, nn * sizeof(DevNode)));
+  YK_HIP(hipMalloc(&t.leaf_geo, count * elem));
+  YK_HIP(hipMalloc(&t.leaf_ids, count * sizeof(uint32_t)));
+  if (!snodes.empty())
+    YK_HIP(hipMemcpy(t.nodes, snodes.data(), snodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
+  YK_HIP(hipMemcpy(t.leaf_geo, leaf_geo.data(), count * elem, hipMemcpyHostToDevice));
+  YK_HIP(hipMemcpy(t.leaf_ids, bvh.order.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
+  t.root = root_code;
+  t.depth = bvh.depth;
+  t.origin_bound = bvh.origin_bound;
+  t.n_nodes = (uint32_t)snodes.size();
+  // LDS layout: [nodes][leaf geometry][leaf ids][traversal stacks]
+  auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+  const size_t scene_bytes = a16(t.n_nodes * sizeof(DevNode)) + a16(count * elem) + a16(count * sizeof(uint32_t));
+  t.in_lds = scene_bytes <= 64 * 1024;
+#if YK_WIDE
+  // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries), but
+  // the stacks share LDS with the scene, so the capacity is what still fits 3 blocks per CU (at
+  // least 8); a lane that would exceed it abandons the traversal for the exact linear scan.
+  // Pushes write unconditionally at the current top (up to 3 past the capacity): +4 entries.
+  {
+    // (2 KB below a third of the CU's LDS: the hardware's allocation granularity — 3 blocks of
+    // 54144 bytes measured only 2 resident per CU, with the grid still sized for 3)
+    const size_t budget = (size_t)160 * 1024 / 3 - 2048;
+    const size_t used = t.in_lds ? scene_bytes : 0;
+    const uint32_t fit = used + 12 * kBlock * 4 <= budget ? (uint32_t)((budget - used) / (kBlock * 4)) : 12u;
+    t.stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
+    t.stack_entries = t.stack_cap + 4;
+  }
+#else
+  t.stack_cap = bvh.depth + 1;
+  t.stack_entries = bvh.depth + 1;
+#endif
+  t.geo_off = (uint32_t)a16(t.n_nodes * sizeof(DevNode));
+  t.ids_off = t.geo_off + (uint32_t)a16(count * elem);
+  t.stack_off = t.in_lds ? (uint32_t)scene_bytes : 0u;
+  t.lds_bytes = t.stack_off + t.stack_entries * kBlock * (uint32_t)sizeof(int32_t);
+  int per_cu = 0;
+  const hipError_t e =
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t.in_lds ? kern_lds : kern_glob, kBlock, t.lds_bytes);
+  if (e != hipSuccess || per_cu < 1) per_cu = 1;
+  t.grid = per_cu * ctx->cus;
+  return YK_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1542,6 +1778,9 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   for (int k16 = 0; k16 < 16; ++k16)
     (void)hipFuncSetAttribute((const void*)fp64_kernel(k16 & 8, k16 & 7), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
+  for (int k8 = 0; k8 < 8; ++k8)
+    (void)hipFuncSetAttribute((const void*)f32_kernel(k8 & 4, (k8 & 1) | ((k8 & 2) << 1)),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
@@ -1568,9 +1807,8 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_order);
   (void)hipFree(ctx->d_col);
   (void)hipFree(ctx->d_acc);
-  (void)hipFree(ctx->d_nodes);
-  (void)hipFree(ctx->d_leaf_geo);
-  (void)hipFree(ctx->d_leaf_ids);
+  ctx->t64.release();
+  ctx->t32.release();
   (void)hipFree(ctx->d_mt);
   (void)hipFree(ctx->d_ids);
   (void)hipFree(ctx->d_rgb);
@@ -1617,84 +1855,30 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   }
   YK_HIP(hipMemcpy(ctx->d_geo, geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
   YK_HIP(hipMemcpy(ctx->d_geo_f, geo_f.data(), count * sizeof(float4), hipMemcpyHostToDevice));
-  // BVH over the spheres (culling only)
+  // the BVHs (culling only): the FP64 kernel's and the FP32 kernel's, whose boxes
+  // also carry render<float>'s sphere-test error (§4.1)
   std::vector<double> centers(3 * size_t(count)), radii(count);
+  double rmin = INFINITY;
   for (uint32_t i = 0; i < count; ++i) {
     for (int k = 0; k < 3; ++k) centers[3 * i + k] = spheres[i].center[k];
     radii[i] = spheres[i].radius;
+    rmin = std::min(rmin, std::fabs(radii[i]));
   }
   double cam_ext = 0;
   for (int k = 0; k < 3; ++k) cam_ext = std::max(cam_ext, std::fabs(camera->origin[k]));
   ykbvh::Options bopt;
   if (const char* e = std::getenv("YKGPU_BVH_LEAF")) bopt.max_leaf = std::max(1, std::min(15, std::atoi(e)));
-  ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, bopt);
-  if (bvh.depth > ykbvh::kMaxDepth) return fail(YK_ERR_INVALID, "BVH deeper than the traversal stack");
-  std::vector<SphereGeo> leaf_geo(count);
-  for (uint32_t i = 0; i < count; ++i) leaf_geo[i] = geo[bvh.order[i]];
-  (void)hipFree(ctx->d_nodes);
-  (void)hipFree(ctx->d_leaf_geo);
-  (void)hipFree(ctx->d_leaf_ids);
-  ctx->d_nodes = nullptr;
-  ctx->d_leaf_geo = nullptr;
-  ctx->d_leaf_ids = nullptr;
-#if YK_WIDE
-  int32_t root_code = 0;
-  uint32_t wdepth = 0;
-  const std::vector<DevNode> snodes = ykbvh::wide_nodes(bvh, &root_code, &wdepth);
-#else
-  const std::vector<DevNode> snodes = ykbvh::slab_nodes(bvh);
-  const int32_t root_code = ykbvh::slab_root(bvh);
-#endif
-  const size_t nn = std::max<size_t>(1, snodes.size());
-  YK_HIP(hipMalloc(&ctx->d_nodes, nn * sizeof(DevNode)));
-  YK_HIP(hipMalloc(&ctx->d_leaf_geo, count * sizeof(SphereGeo)));
-  YK_HIP(hipMalloc(&ctx->d_leaf_ids, count * sizeof(uint32_t)));
-  if (!snodes.empty())
-    YK_HIP(hipMemcpy(ctx->d_nodes, snodes.data(), snodes.size() * sizeof(DevNode),
-                     hipMemcpyHostToDevice));
-  YK_HIP(hipMemcpy(ctx->d_leaf_geo, leaf_geo.data(), count * sizeof(SphereGeo), hipMemcpyHostToDevice));
-  YK_HIP(hipMemcpy(ctx->d_leaf_ids, bvh.order.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
-  ctx->bvh_root = root_code;
-  ctx->bvh_depth = bvh.depth;
-  ctx->origin_bound = bvh.origin_bound;
-  ctx->n_nodes = (uint32_t)snodes.size();
-  // LDS layout: [nodes][leaf geometry][leaf ids][traversal stacks]
-  auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-  const size_t scene_bytes = a16(ctx->n_nodes * sizeof(DevNode)) + a16(count * sizeof(SphereGeo)) +
-                             a16(count * sizeof(uint32_t));
-  ctx->scene_in_lds = scene_bytes <= 64 * 1024;
-#if YK_WIDE
-  // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries), but
-  // the stacks share LDS with the scene, so the capacity is what still fits 3 blocks per CU (at
-  // least 8); a lane that would exceed it abandons the traversal for the exact linear scan.
-  // Pushes write unconditionally at the current top (up to 3 past the capacity): +4 entries.
-  {
-    // (2 KB below a third of the CU's LDS: the hardware's allocation granularity — 3 blocks of
-    // 54144 bytes measured only 2 resident per CU, with the grid still sized for 3)
-    const size_t budget = (size_t)160 * 1024 / 3 - 2048;
-    const size_t used = ctx->scene_in_lds ? scene_bytes : 0;
-    const uint32_t fit = used + 12 * kBlock * 4 <= budget ? (uint32_t)((budget - used) / (kBlock * 4)) : 12u;
-    ctx->stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
-    ctx->stack_entries = ctx->stack_cap + 4;
-  }
-#else
-  ctx->stack_cap = bvh.depth + 1;
-  ctx->stack_entries = bvh.depth + 1;
-#endif
-  ctx->lds_geo_off = (uint32_t)a16(ctx->n_nodes * sizeof(DevNode));
-  ctx->lds_ids_off = ctx->lds_geo_off + (uint32_t)a16(count * sizeof(SphereGeo));
-  ctx->lds_stack_off = ctx->scene_in_lds ? (uint32_t)scene_bytes : 0u;
-  ctx->lds_bytes = ctx->lds_stack_off + ctx->stack_entries * kBlock * (uint32_t)sizeof(int32_t);
-  int per_cu = 0;
-  hipError_t e = ctx->scene_in_lds
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<true, 0>, kBlock, ctx->lds_bytes)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, yk_render_persistent<false, 0>, kBlock, ctx->lds_bytes);
-  if (e != hipSuccess || per_cu < 1) per_cu = 1;
-  ctx->grid = per_cu * ctx->cus;
-  int per_cu_f = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_f, yk_render_f32<0>, kBlock, 0);
-  if (e != hipSuccess || per_cu_f < 1) per_cu_f = 1;
-  ctx->grid_f32 = per_cu_f * ctx->cus;
+  int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, geo.data(), sizeof(SphereGeo),
+                       fp64_kernel(true, 0), fp64_kernel(false, 0));
+  if (rc) return rc;
+  ykbvh::Options fopt = bopt;
+  fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
+  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4),
+                   f32_kernel(true, 0), f32_kernel(false, 0));
+  if (rc) return rc;
+  // the float bound assumes neither underflow nor overflow: a scene outside that
+  // scale renders FP32 with the linear scan throughout
+  if (!(rmin >= 0x1p-20) || !(ctx->t32.origin_bound <= 0x1p20)) ctx->t32.origin_bound = -1.0;
   YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));
   ctx->nspheres = count;
   ctx->cam = *camera;
