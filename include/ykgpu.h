@@ -50,7 +50,8 @@ enum { YK_MATERIAL_LAMBERTIAN = 0, YK_MATERIAL_METAL = 1, YK_MATERIAL_DIELECTRIC
  * and camera vectors are the records' doubles rounded to float.  (As shipped, render<float>
  * does not compile — sphere's deduction guide rejects the double radius literals — so FP32 is
  * pinned against the reference's headers with the literals written as T(...): DESIGN.md §2.)
- * FP32 uses the linear closest-hit scan (the BVH culling proof of DESIGN.md §4 is for FP64). */
+ * FP32 has its own BVH, whose boxes and per-ray cone carry the float sphere test's proven error
+ * (DESIGN.md §4.1): its images equal the linear scan's bit for bit. */
 enum { YK_PRECISION_FP64 = 0, YK_PRECISION_FP32 = 1 };
 
 /* Per-sample engine (the Engine of source.cpp:155/159, seeded per sample as yk_render_params.
