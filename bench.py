@@ -77,6 +77,8 @@ def parse():
                     help="CPU baseline renders every k-th row at full spp")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-modes", action="store_true",
+                    help="skip the one-call timings of the FP32 and xor128 modes (rank 0, N=1)")
     return ap.parse_args()
 
 
@@ -301,6 +303,25 @@ def main():
             "max_abs_levels": int(np.abs(gpu_rows.astype(int) - cpu_rgb.astype(int)).max()),
             "bytes_differing": int((gpu_rows != cpu_rgb).sum()),
         }
+
+    if rank == 0 and world == 1 and not args.no_modes:
+        # The reference's other arithmetic and engine on the same workload, after everything
+        # above: render<float> (its own tree) and the yk::xor128 engine.  Each is
+        # bit-exact against the reference in its own mode; neither is the contract's `value`.
+        from uecraytracing_amd.records import PRECISION_FP32, RNG_XOR128
+        scratch = torch.empty_like(tg.tile)
+        modes = {}
+        for name, kw in (("fp32_mt19937", {"precision": PRECISION_FP32}), ("fp64_xor128", {"rng": RNG_XOR128})):
+            mp = make_params(W, H, spp, depth, args.seed0, rows=tile_rows(rank, world, H), **kw)
+            ren.render_async(mp, scratch.data_ptr(), stream.cuda_stream)  # warm-up call
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            ren.render_async(mp, scratch.data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            modes[name] = {"value": round(total_samples / dt / 1e6, 3), "unit": "Msamples/s",
+                           "ms": round(dt * 1e3, 3)}
+        result["modes"] = modes
 
     if rank == 0:
         print(json.dumps(result), flush=True)

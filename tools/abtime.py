@@ -2,7 +2,7 @@
 instance, flags=0): one subprocess per variant run (one library per process), interleaved.
 usage: python tools/abtime.py <spp> <variant> [<variant> ...]   (variant 'base' = lib/libykgpu.so,
 otherwise lib/abl/libykgpu_<variant>.so); AB_ROWS="begin:count:stride" renders a row tile only
-(e.g. "0:135:8" = rank 0 of 8)"""
+(e.g. "0:135:8" = rank 0 of 8); AB_PREC=1 times the FP32 mode"""
 import json
 import os
 import subprocess
@@ -18,7 +18,7 @@ from uecraytracing_amd.records import make_params
 arr, cam = yk.build_scene("final", 42)
 r = yk.Renderer(0); r.set_scene(arr, cam)
 rows = tuple(int(v) for v in sys.argv[3].split(":")) if len(sys.argv) > 3 and sys.argv[3] else None
-p = make_params(1920, None, int(sys.argv[1]), 50, 404, rows=rows, flags=0)
+p = make_params(1920, None, int(sys.argv[1]), 50, 404, rows=rows, flags=0, precision=int(sys.argv[4]))
 img = r.render(p); ts = []
 for _ in range(int(sys.argv[2])):
     t = time.perf_counter(); r.render(p); ts.append(time.perf_counter() - t)
@@ -34,7 +34,8 @@ for rnd in range(2):
         lib = os.path.join(ROOT, "uecraytracing_amd/lib/libykgpu.so") if name == "base" else \
             os.path.join(ROOT, f"uecraytracing_amd/lib/abl/libykgpu_{name}.so")
         env = dict(os.environ, YKGPU_LIB_OVERRIDE=lib)
-        out = subprocess.run([sys.executable, "-c", CODE, spp, reps, os.environ.get("AB_ROWS", "")],
+        out = subprocess.run([sys.executable, "-c", CODE, spp, reps, os.environ.get("AB_ROWS", ""),
+                              os.environ.get("AB_PREC", "0")],
                              env=env, capture_output=True, text=True)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         print(rnd, name, line[-1] if line else out.stderr[-400:], flush=True)
