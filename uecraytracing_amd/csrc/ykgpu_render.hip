@@ -558,7 +558,9 @@ void yk_render_persistent(KernelArgs ka) {
         // candidate lower bounds kept as floats rounded down, compared with ustar_f (>= U*):
         // both only ever keep MORE candidates than the double comparison would
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-        bool overflow = false;
+        // a VGPR, not a bool: a bool carried round the traversal loop lives in a lane mask that
+        // every divergent exit has to merge (-3.4% render time as an integer)
+        uint32_t overflow = 0;
         int32_t node = ka.bvh_root;
 #if YK_WIDE
         int32_t* top = stk;  // this lane's traversal stack top (entries kBlock words apart)
@@ -1030,7 +1032,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
         const char* const pz = nodes + 96u + (d.z < 0.0f ? 16u : 0u);
         const float tmin_lo = tmin * (1.0f - 0x1p-17f);
         float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
-        uint32_t overflow = 0;  // (a VGPR, not a lane-mask bool, across the loop's divergent exits)
+        uint32_t overflow = 0;  // a VGPR, not a lane-mask bool (see the FP64 kernel)
         int32_t node = ka.bvh_root;
         int32_t* top = stk;
         const int32_t* const stk_cap = stk + ka.stack_cap * kBlock;
