@@ -12,7 +12,7 @@
 //   * yk_render_persistent is one persistent grid over SAMPLE SLOTS: a lane runs one path at a
 //     time, one SEGMENT (closest hit + scatter) per trip round the loop, writes the sample's
 //     colour when the path ends and takes the next slot from a wave-level reserve (one atomic
-//     per 128 slots) — active-lane refill, so no lane idles while the launch has slots.
+//     per 512 slots) — active-lane refill, so no lane idles while the launch has slots.
 //   * the colour of a path is attenuation_1 * (attenuation_2 * (... * L)): double
 //     multiplication does not associate, so the lane keeps the ids of the scattering spheres
 //     on a small stack (8 in registers, the rest in a per-lane global spill) and multiplies
@@ -111,7 +111,10 @@ constexpr int kCounters = 24;  // [16..18]: timeline, [19..22]: diag (diagnostic
   } while (0)
 #endif
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
-constexpr uint32_t kClaim = 128;    // sample slots a wave claims per atomic
+#ifndef YK_CLAIM
+#define YK_CLAIM 512
+#endif
+constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
 #define YK_STR2(x) #x
 #define YK_STR(x) YK_STR2(x)
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
@@ -657,6 +660,9 @@ void yk_render_persistent(KernelArgs ka) {
           } else {
             YK_STAMP(2);  // interior nodes since the last stamp
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
+#ifdef YK_LEAF_UNROLL
+#pragma unroll YK_LEAF_UNROLL
+#endif
             for (uint32_t k = 0; k < cnt; ++k) {
               const SphereGeo sg = leaf_geo[first + k];
               ++n_test;
