@@ -6,7 +6,8 @@ proven bound: a root the float test accepts puts the exact point o + r d within
 2^-8.9 (|o - c| + R) of the float sphere, hence within 2^-8.9 (r |d| + 2R).  This replays the test
 in numpy float32 (same operations in the same order, no FMA; the reference's Newton square root
 from the oracle) on rays aimed at silhouettes and surfaces over four decades of scale, and checks
-both forms of the bound and the cone constant's margin over them.
+its three forms (linear, cone,
+quadratic) and the margins of the constants built on them.
 """
 import numpy as np
 
@@ -14,6 +15,8 @@ import oracle_lib
 
 BOUND = 2.0 ** -8.9
 K_F32_CONE = 2.0 ** -8 * (1 + 2.0 ** -10)  # yk_bvh.hpp kF32Cone
+QUAD = 72.7 * 2.0 ** -24                   # dev <= QUAD (|o - c|^2 + R^2) / R, DESIGN.md §4.1
+K_F32_BIG_GROW = 2.0 ** -15                # yk_bvh.hpp kF32BigGrow
 F = np.float32
 
 
@@ -63,7 +66,7 @@ def near_tangent_rays(rng, n):
 
 def test_float_sphere_test_error_bound():
     rng = np.random.default_rng(20261016)
-    worst, worst_cone, accepted = 0.0, 0.0, 0
+    worst, worst_cone, worst_quad, accepted = 0.0, 0.0, 0.0, 0
     for _ in range(4):
         o, d, c, R = near_tangent_rays(rng, 250_000)
         r, ok = float_test(o, d, c, R)
@@ -75,8 +78,12 @@ def test_float_sphere_test_error_bound():
         dn = np.linalg.norm(d64, axis=1)
         worst = max(worst, float(np.max(np.where(ok, dev / (oc + rad), 0.0))))
         worst_cone = max(worst_cone, float(np.max(np.where(ok, dev / (r * dn + 2 * rad), 0.0))))
+        # the quadratic form the big-sphere growth rests on (yk_bvh.hpp kF32BigGrow)
+        worst_quad = max(worst_quad, float(np.max(np.where(ok, dev * rad / (oc ** 2 + rad ** 2), 0.0))))
         accepted += int(ok.sum())
     assert accepted > 300_000
     assert worst <= BOUND, np.log2(worst)
     assert worst_cone <= BOUND, np.log2(worst_cone)
     assert K_F32_CONE >= 1.85 * BOUND
+    assert worst_quad <= QUAD, worst_quad / QUAD
+    assert K_F32_BIG_GROW / 2 >= 3.5 * QUAD

@@ -141,7 +141,14 @@ Built build(const double* centers, const double* radii, uint32_t n, double camer
     bd.idx.resize(n);
     std::iota(bd.idx.begin(), bd.idx.end(), 0u);
     for (uint32_t i = 0; i < n; ++i) {
-      const double r = std::fabs(radii[i]) * (1.0 + opt.radius_grow) + out.delta;
+      const double ar = std::fabs(radii[i]);
+      double g = ar * opt.radius_grow;
+      if (opt.f32_big) {
+        const double* c = centers + 3 * i;
+        const double reach = std::sqrt(3.0) * out.origin_bound + std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) + ar;
+        if (kF32BigReach * ar >= reach * (1.0 + 0x1p-20)) g = std::min(g, ar * kF32BigGrow);
+      }
+      const double r = ar + g + out.delta;
       for (int k = 0; k < 3; ++k) {
         bd.sbox[i].lo[k] = centers[3 * i + k] - r;
         bd.sbox[i].hi[k] = centers[3 * i + k] + r;

@@ -61,6 +61,13 @@ constexpr int32_t kEmptyLeaf = ~0;  // leaf code with no spheres
 // by 2 kF32Cone |radius| on top of delta, and the FP32 kernel widens every ray into a cone of
 // slope kF32Cone |d|: 1.87x the bound.
 constexpr float kF32Cone = 0x1p-8f * (1.0f + 0x1p-10f);
+// A sphere that every hit distance stays within kF32BigReach radii of (kF32BigReach |radius| >=
+// sqrt(3) origin_bound + |c| + |radius|) needs far less: the bound's quadratic form,
+// 72.7 u (t^2 |d|^2 / R + 2 t |d| + 2 R) with u = 2^-24, stays below
+// kF32Cone t |d| + kF32BigGrow |radius| there (3.5x margin on 72.7 u).  The RTIOW ground sphere
+// (r = 1000) then grows by 0.03 instead of 7.8.
+constexpr double kF32BigGrow = 0x1p-15;
+constexpr double kF32BigReach = 192.0;
 
 struct Built {
   std::vector<Node> nodes;      // nodes[0] is the root when root >= 0
@@ -75,6 +82,7 @@ struct Options {
   uint32_t max_leaf = 2;  // spheres per leaf (<= 15); 2 measured best on the final scene
   int bins = 16;          // SAH bins per split
   double radius_grow = 0; // extra box growth per unit |radius| (FP32 trees: 2 kF32Cone)
+  bool f32_big = false;   // FP32 trees: kF32BigGrow for spheres within kF32BigReach radii
 };
 
 // centers: 3 doubles per sphere; radii may be negative (hollow shells: |r| is used).

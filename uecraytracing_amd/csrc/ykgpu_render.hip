@@ -1881,6 +1881,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
   fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
+  fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
   rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4),
                    f32_kernel(true, 0), f32_kernel(false, 0));
   if (rc) return rc;
