@@ -1388,7 +1388,10 @@ constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
 // launch c - ring.  With the whole call in the ring (1920x1080x512: 4.25 GB) every warm-up is
 // queued at once and none waits for a render to end.
 constexpr uint64_t kWarmBytes = 8ull << 30;
-constexpr uint32_t kFirstLaunch = 8;  // samples per pixel in the first launch
+#ifndef YK_FIRST_LAUNCH
+#define YK_FIRST_LAUNCH 8
+#endif
+constexpr uint32_t kFirstLaunch = YK_FIRST_LAUNCH;  // samples per pixel in the first launch
 #ifndef YK_TILE
 #define YK_TILE 8
 #endif
