@@ -11,10 +11,14 @@ N), each rank renders its tile into device memory, and the tiles are gathered to
 RCCL (torch.distributed 'nccl') and de-interleaved on device — all inside the timed region.
 The total image is fixed, so this is STRONG scaling.
 
-Prints ONE JSON line on rank 0.  The `roofline` object is computed from HIP events recorded on
-the render stream around every timed launch and the kernel's own work counters; the
-`cpu_baseline` is the CPU oracle restatement (oracle/yk_oracle.c, "port") on a strided row
-subset of the same workload, on this host's cores, rank 0 at N=1 only.
+Prints ONE JSON line on rank 0.  The `roofline` object is the dominant kernel's VALU roofline
+(the path is neither HBM- nor MFMA-bound): algorithmic FP64 flops per launch (the
+reference's expressions over the kernel's own work counters, uecraytracing_amd/flops.py) over the
+launch duration = the union of the launches' HIP-event spans / launches (they overlap on two
+streams, so a per-span average would count the overlap twice).  HBM and issue views sit beside
+it.  The `cpu_baseline` is the CPU oracle restatement (oracle/yk_oracle.c, "port") on a strided
+row subset of the same workload, on every CPU this job may use (the box's cgroup quota), rank 0
+at N=1 only.
 """
 from __future__ import annotations
 
@@ -30,15 +34,41 @@ sys.path.insert(0, ROOT)
 METRIC = "Msamples/sec at 1920x1080x512spp (~500 spheres); per-pixel RMSE vs CPU"
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP32 vector 157.3 TF / 2, MI355X_MICROARCH.md)
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
-# Algorithmic FP64 flops per work unit, counted from the reference's arithmetic:
-FLOPS_PER_SPHERE_TEST = 17    # sphere.hpp:29-33 discriminant: 3 sub, 2 dots (3 mul+2 add), 1 sub, 2 mul+1 sub
-FLOPS_PER_ROOT = 4            # sphere.hpp:36-39: (-hb -/+ sq) / a, one or two roots
-FLOPS_PER_NEWTON_ITER = 3     # math.hpp:14-17: s/x, x + ., ./2
-FLOPS_PER_SEGMENT = 40        # |d|^2, hit record (p, normal, face: 17), normalize (8), scatter (~10)
-FLOPS_PER_SAMPLE = 30         # jitter + camera ray (24), accumulate + attenuation products (~6)
-
+SPHERE_RECORD_BYTES = 80      # yk_sphere (include/ykgpu.h): the scene a workgroup stages once
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+FP64_RECONCILE = os.path.join(ROOT, "profiles", "r02_fp64_reconcile.json")
+
+
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, capped by the cgroup CPU quota (the GPU
+    box grants each one-GPU job 16 of the node's 256 logical CPUs), and the node's count."""
+    node = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else node
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    if quota is not None:
+        n = max(1, min(n, int(quota)))
+    return n, node, quota
+
+
+def fp64_reconcile_facts():
+    """The committed FP64 counter reconciliation (tools/gpu_fp64_reconcile.sh), or None."""
+    if not os.path.exists(FP64_RECONCILE):
+        return None
+    with open(FP64_RECONCILE) as f:
+        rec = json.load(f)
+    keep = ("workload", "implementation_model_vs_counter", "algorithmic_share_of_executed",
+            "fp64_lane_utilization", "per_sample")
+    out = {k: rec[k] for k in keep if k in rec}
+    out["source"] = "profiles/r02_fp64_reconcile.json (tools/gpu_fp64_reconcile.sh)"
+    out["calibration"] = rec.get("calibration", {}).get("finding")
+    return out
 
 
 def pmc_facts(workload=None):
@@ -56,12 +86,6 @@ def pmc_facts(workload=None):
     return {k: rec[k] for k in keep if k in rec}
 
 
-def fp64_flops(st):
-    return (st["sphere_tests"] * FLOPS_PER_SPHERE_TEST + st["sqrt_calls"] * FLOPS_PER_ROOT
-            + st["newton_calls"] + st["newton_iters"] * FLOPS_PER_NEWTON_ITER
-            + st["segments"] * FLOPS_PER_SEGMENT + st["samples"] * FLOPS_PER_SAMPLE)
-
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,7 +99,8 @@ def parse():
     ap.add_argument("--seed0", type=int, default=404)
     ap.add_argument("--cpu-row-step", type=int, default=45,
                     help="CPU baseline renders every k-th row at full spp")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: every CPU this job may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-modes", action="store_true",
                     help="skip the one-call timings of the FP32 and xor128 modes (rank 0, N=1)")
@@ -94,6 +119,7 @@ def main():
     import torch.distributed as dist
 
     import uecraytracing_amd as yk
+    from uecraytracing_amd import flops
     from uecraytracing_amd.records import image_height_for, make_params
     from uecraytracing_amd.tiles import TileGather, tile_rows
 
@@ -125,7 +151,15 @@ def main():
     params = make_params(W, H, spp, depth, args.seed0, rows=rows, flags=0)  # production instance
 
     ren = yk.Renderer(local)
-    ren.set_scene(spheres, cam)  # world + camera uploaded to HBM before any timing
+    # world + camera uploaded to HBM before any timing (the contract: inputs resident when the
+    # timed region starts); SURVEY §8(d) counts the upload in the render call, so its cost (host
+    # BVH builds + H2D copies, per rank) is timed here and reported beside the step
+    up = []
+    for _ in range(3):
+        t = time.perf_counter()
+        ren.set_scene(spheres, cam)
+        up.append((time.perf_counter() - t) * 1e3)
+    scene_upload_ms = sorted(up)[1]
     stream = torch.cuda.Stream(device=dev)
     tg = TileGather(rank, world, H, W, dev)  # tile, gather buffers and the assembled image
     ev = []
@@ -162,7 +196,6 @@ def main():
 
     call_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     tst = ren.stats()  # per-kernel event timings of the last timed step (same stream)
-    kernel_ms = tst["kernel_ms"]  # the render kernel, summed over its launches in one step
     launches = max(1, tst["launches"])
     # work counters: one more launch of the same workload with the counting instance, after the
     # timed region (the work is deterministic, so its counts are the timed launches' counts)
@@ -172,19 +205,32 @@ def main():
     st = ren.stats()
     total_samples = W * H * spp
     value = total_samples * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel (yk_render_persistent, `launches` launches per step):
-    # algorithmic FP64 flops of the arithmetic it executed per launch (its own unit counters,
-    # / launches) over its average launch duration (HIP events around each launch)
-    flops = fp64_flops(st)
-    launch_ms = kernel_ms / launches
-    achieved_tf = (flops / launches) / (launch_ms * 1e-3) / 1e12
-    # algorithmic HBM bytes of the render kernel per step: x_397 in (4 B) + colour out (24 B)
-    # per sample, the scene once per launch
-    hbm_bytes = rows_mine * W * spp * (4 + 24) + launches * len(spheres) * 96
+    # Roofline of the dominant kernel, yk_render_persistent (`launches` launches per step).
+    # Launch c + 1 starts on the CUs launch c's draining blocks free (two streams), so spans
+    # overlap: the per-launch duration is the UNION of the spans / launches, never their sum.
+    busy_ms = tst["render_busy_ms"]
+    launch_ms = busy_ms / launches
+    alg = flops.algorithmic(st)       # FP64 flops of the reference's expressions, per step
+    impl = flops.implementation(st)   # counter-weighted FP64 operations the kernel executes
+    achieved_tf = alg / launches / (launch_ms * 1e-3) / 1e12
+    impl_tf = impl / launches / (launch_ms * 1e-3) / 1e12
+    # SURVEY §8(d) algorithmic HBM bytes: the RGB8 image once, the scene once per workgroup
+    scene_bytes = len(spheres) * SPHERE_RECORD_BYTES
+    hbm_step = rows_mine * W * 3 + launches * tst["grid_blocks"] * scene_bytes
+    hbm_gbps = hbm_step / launches / (launch_ms * 1e-3) / 1e9
     workload = f"{args.scene}{args.scene_seed}_{W}x{H}x{spp}_d{depth}_n{world}"
     facts = pmc_facts(workload)
     traffic = facts.get("hbm_bytes_per_launch") if facts else None
+    issue = None
+    if facts and "valu_pipe_util" in facts and "valu_lane_utilization" in facts:
+        issue = {"valu_busy": round(facts["valu_pipe_util"], 4),
+                 "lane_utilization": round(facts["valu_lane_utilization"], 4),
+                 "busy_x_lanes": round(facts["valu_pipe_util"] * facts["valu_lane_utilization"], 4),
+                 "source": "PMC (profiles/pmc_summary.json): VALU busy = SQ_INSTS_VALU x 2 cycles "
+                           "(SIMD-32) / GRBM_GUI_ACTIVE per XCD; lanes = SQ_THREAD_CYCLES_VALU / "
+                           "(64 SQ_ACTIVE_INST_VALU)"}
 
     result = {
         "metric": METRIC,
@@ -193,7 +239,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -205,45 +251,50 @@ def main():
                         f"seed0 {args.seed0}, mt19937 + FP64 bit-exact",
             "image": f"{W}x{H}", "spp": spp, "max_depth": depth, "spheres": len(spheres),
             "scene_file": os.path.relpath(scene_file, ROOT) if scene_file else None,
-            "partition": f"cyclic rows over {world} GPU(s), RCCL gather to rank 0",
+            "partition": f"cyclic 8-row bands over {world} GPU(s), RCCL gather to rank 0",
         },
-        # The contract's roofline is HBM or MFMA.  This kernel is neither HBM- nor MFMA-bound (no
-        # dense contraction; ~1.4% of HBM peak): it is bound by VALU issue under divergence
-        # (DESIGN.md §5), so the HBM view is the contract's line and the FP64 VALU view sits
-        # beside it under "valu".
+        "scene_upload_ms": round(scene_upload_ms, 3),
+        "value_incl_scene_upload": round(total_samples * args.steps
+                                         / (elapsed + args.steps * scene_upload_ms * 1e-3) / 1e6, 3),
+        # the path is VALU-bound (FP64 vector arithmetic under divergence), neither
+        # HBM- nor MFMA-bound; the HBM view is a sub-object
         "roofline": {
-            "bound": "hbm",
-            "achieved": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 3),
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+            "bound": "valu",
+            "achieved": round(achieved_tf, 4),
+            "peak": FP64_VALU_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 5),
             "traffic": traffic,
-            "algorithmic_bytes_per_launch": round(hbm_bytes / launches),
-            "algorithmic": "28 B per sample (x_397 word in, 3 x f64 colour out) + the scene once "
-                           "per launch; traffic = PMC HBM bytes per launch (FETCH_SIZE x2 + "
-                           "WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction)",
             "kernel": "yk_render_persistent",
             "launches_per_step": launches,
-            "avg_launch_ms": round(launch_ms, 3),
-            "note": "not HBM- or MFMA-bound: VALU issue and divergence (valu, pmc)",
-            # render = the launches' spans summed (consecutive launches overlap: launch c + 1
-            # takes the CUs launch c's draining blocks free); render_busy = their union
-            "step_breakdown_ms": {"render": round(kernel_ms, 3), "render_busy": round(tst["render_busy_ms"], 3),
+            "launch_ms": round(launch_ms, 4),
+            "launch_ms_source": "union of the launches' HIP-event spans (render_busy_ms) / launches",
+            "algorithmic_flops_per_launch": round(alg / launches),
+            "algorithmic": f"FP64 flops of the reference's expressions, {flops.algorithmic_terms()}, "
+                           f"over the kernel's work counters: {alg:.5g} per step / {launches} launches",
+            "implementation": {
+                "flops_per_launch": round(impl / launches),
+                "achieved": round(impl_tf, 4),
+                "frac": round(impl_tf / FP64_VALU_PEAK_TFLOPS, 5),
+                "note": "FP64 operations the kernel executes (divisions as rcp+FMA sequences, "
+                        "math::sqrt's start and steps, the BVH's root bounds), weighted as "
+                        "SQ_INSTS_VALU_FLOPS_FP64 weighs them (uecraytracing_amd/flops.py)",
+                "counter_check": fp64_reconcile_facts(),
+            },
+            "issue": issue,
+            "hbm": {"algorithmic_bytes_per_launch": round(hbm_step / launches),
+                    "achieved": round(hbm_gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(hbm_gbps / HBM_PEAK_GBPS, 7), "traffic": traffic,
+                    "algorithmic": f"SURVEY §8(d): the RGB8 image ({rows_mine * W * 3} B) once per "
+                                   f"step + the scene ({scene_bytes} B) once per workgroup "
+                                   f"({tst['grid_blocks']} per launch); traffic = PMC FETCH_SIZE x2 + "
+                                   f"WRITE_SIZE per launch (scratch: colours, x_397, MT state)"},
+            "checks": {"launches_x_launch_ms_le_step": bool(launches * launch_ms <= ms_per_step * 1.001)},
+            # render = the launches' spans summed (they overlap); render_busy = their union
+            "step_breakdown_ms": {"render_spans_summed": round(tst["kernel_ms"], 3),
+                                  "render_busy": round(busy_ms, 3),
                                   "mt_warmup": round(tst["warmup_ms"], 3),
                                   "reduce": round(tst["resolve_ms"], 3), "call": round(call_ms, 3)},
-            "valu": {
-                "achieved": round(achieved_tf, 3),
-                "peak": FP64_VALU_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 4),
-                "algorithmic": (f"FP64 flops of the reference arithmetic executed per step = "
-                                f"{FLOPS_PER_SPHERE_TEST}/sphere test x {st['sphere_tests']} + "
-                                f"{FLOPS_PER_ROOT}/exact root x {st['sqrt_calls']} + math::sqrt "
-                                f"(1/call x {st['newton_calls']} + {FLOPS_PER_NEWTON_ITER}/iteration x "
-                                f"{st['newton_iters']}) + {FLOPS_PER_SEGMENT}/segment x "
-                                f"{st['segments']} + {FLOPS_PER_SAMPLE}/sample x {st['samples']} = "
-                                f"{flops:.4g}, / {launches} launches"),
-            },
             "pmc": facts,
             "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
             "tests_per_segment": round(st["sphere_tests"] / max(1, st["segments"]), 2),
@@ -259,7 +310,8 @@ def main():
         import oracle_lib
 
         rows = list(range(0, H, args.cpu_row_step))
-        nthreads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        usable, node_cpus, quota = usable_cpus()
+        nthreads = args.cpu_threads or usable
         cp = make_params(W, H, spp, depth, args.seed0,
                          rows=(0, len(rows), args.cpu_row_step))
         t = time.perf_counter()
@@ -276,6 +328,10 @@ def main():
             "sample": f"{len(rows)} rows (every {args.cpu_row_step}th) x {W} px x {spp} spp = "
                       f"{n} samples of the same workload, {dt:.1f} s, oracle/yk_oracle.c "
                       f"(-O2, {nthreads} threads)",
+            "host": {"node_logical_cpus": node_cpus, "cgroup_cpu_quota": quota,
+                     "threads_used": nthreads,
+                     "note": "threads = every CPU this job may use (affinity capped by the cgroup "
+                             "quota); the node's other CPUs belong to other jobs"},
         }
         # SURVEY §8(d) variants: the same port on ONE core (one row), and the reference's
         # as-shipped cost model (a random_device seed per sample, source.cpp:159) on all threads

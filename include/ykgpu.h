@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 5u
+#define YKGPU_ABI_VERSION 6u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 and DIELECTRIC are extensions needed by BASELINE configs 2-5 (no
@@ -77,8 +77,12 @@ enum { YK_SEED_COUNTER = 0, YK_SEED_RANDOM_DEVICE = 1 };
 /* yk_render_params.flags */
 enum {
   YK_FLAG_COUNT_WORK = 1u, /* count segments / sphere tests (ykgpu_get_stats)              */
-  YK_FLAG_LINEAR_SCAN = 2u /* closest hit by the reference's linear scan instead of the BVH
+  YK_FLAG_LINEAR_SCAN = 2u, /* closest hit by the reference's linear scan instead of the BVH
                               (same results; A/B and debugging)                              */
+  YK_FLAG_ONE_LANE = 4u     /* with COUNT_WORK, FP64 only (diagnostic): one lane per wave runs
+                              paths, the other 63 idle.  The profiler's per-wave-instruction
+                              counters (SQ_INSTS_VALU_FLOPS_FP64 ...) then read exactly the
+                              instructions one lane executed: DESIGN.md §5 reconciliation   */
 };
 
 enum {
@@ -165,6 +169,10 @@ typedef struct yk_render_stats {
   uint32_t grid_blocks;    /* persistent grid size                                     */
   double render_busy_ms;   /* union of the path-tracing launches' spans (wall time with at
                               least one launch running)                                 */
+  uint64_t work[8];        /* flag COUNT_WORK, FP64 (the FP64 flop model):
+                              [0] leaf tests with disc >= 0 (root bounds computed), hits
+                              shaded as [1] lambertian, [2] metal, [3] of them fuzzy,
+                              [4] dielectric; [5..7] 0                                   */
 } yk_render_stats;
 
 typedef struct ykgpu_context ykgpu_context;
@@ -177,7 +185,9 @@ int ykgpu_context_create(int device, ykgpu_context** out);
 int ykgpu_context_destroy(ykgpu_context* ctx);
 
 /* Uploads the world (tuple order) and the camera to HBM.  Replaces building `world` and `cam`
- * inside render() (source.cpp:100-112). */
+ * inside render() (source.cpp:100-112).  Synchronous: first waits for the device (a render
+ * still running from ykgpu_render_async reads the previous scene), then builds the BVHs on the
+ * host and copies them with the spheres. */
 int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count,
                     const yk_camera* camera);
 

@@ -1,0 +1,60 @@
+"""The bench line's roofline recomputes from the committed evidence (CPU; profiles/).
+
+* the FP64 implementation model (uecraytracing_amd/flops.py) agrees with the hardware counter
+  read on a one-lane-per-wave launch (profiles/r02_fp64_reconcile.json) within 1.5x;
+* the latest committed bench line: launches x launch_ms <= ms_per_step (the per-launch duration
+  counts overlapping spans once), `achieved` = algorithmic flops per launch / launch_ms, and the
+  rocprofv3 kernel trace of the same build gives the same per-launch duration within 5%.
+"""
+import glob
+import json
+import os
+
+import pytest
+
+from uecraytracing_amd import flops
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "profiles")
+
+
+def latest(pattern):
+    files = sorted(glob.glob(os.path.join(PROF, pattern)))
+    if not files:
+        pytest.skip(f"no {pattern} in profiles/")
+    return files[-1]
+
+
+def test_fp64_counter_reconciles_with_the_implementation_model():
+    rec = json.load(open(os.path.join(PROF, "r02_fp64_reconcile.json")))
+    st = rec["work"]
+    impl = flops.implementation(st)
+    counter = rec["executed_fp64_one_lane_counter"]
+    assert 1 / 1.5 < impl / counter < 1.5
+    # the algorithmic model is a subset of what executes; lane-slots issued bound it from above
+    assert flops.algorithmic(st) < counter < rec["issued_lane_slots_fp64"]
+    # the calibration found the counter per wave-instruction, independent of the exec mask
+    fma = [c for c in rec["calibration"]["cases"] if c["op"] == "fma_f64"]
+    assert {c["active_lanes"] for c in fma} == {64, 16}
+    assert all(abs(c["flops_fp64_per_wave_instr"] - 2.0) < 0.01 for c in fma)
+
+
+def test_bench_roofline_is_admissible():
+    b = json.load(open(latest("r0*_bench.json")))
+    rf = b["roofline"]
+    assert rf["bound"] == "valu"
+    assert rf["launches_per_step"] * rf["launch_ms"] <= b["ms_per_step"] * 1.001
+    ach = rf["algorithmic_flops_per_launch"] / (rf["launch_ms"] * 1e-3) / 1e12
+    assert abs(ach - rf["achieved"]) / rf["achieved"] < 0.01
+    assert abs(rf["achieved"] / rf["peak"] - rf["frac"]) / rf["frac"] < 0.01
+
+
+def test_rocprof_union_agrees_with_bench_launch_ms():
+    bench = latest("r0*_bench.json")
+    tag = os.path.basename(bench)[: -len("_bench.json")]
+    union = os.path.join(PROF, f"{tag}_kernel_union.json")
+    if not os.path.exists(union):
+        pytest.skip("no kernel trace union for the latest bench")
+    b = json.load(open(bench))
+    u = json.load(open(union))
+    assert abs(u["union_per_dispatch_ms"] - b["roofline"]["launch_ms"]) / b["roofline"]["launch_ms"] < 0.05

@@ -1,0 +1,56 @@
+"""FP64 flop reconciliation of yk_render_persistent.
+
+Run under rocprofv3 with the FP64 counters (tools/gpu_fp64_reconcile.sh).  Renders the bench
+workload's scene and image (final42, 1920x1080) at `--spp` samples with the counting instance
+twice, in this order:
+  call 0: all 64 lanes of every wave (YK_FLAG_COUNT_WORK);
+  call 1: one lane per wave (YK_FLAG_COUNT_WORK | YK_FLAG_ONE_LANE) — the per-wave-instruction
+          counters then count exactly the FP64 operations the lanes executed.
+Both calls render the same samples (same seeds), so their work counters must agree; the JSON on
+stdout carries both calls' counters for tools/fp64_reconcile_summary.py.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch  # noqa: F401  (torch's HIP runtime first, uecraytracing_amd/__init__.py)
+
+    import uecraytracing_amd as yk
+    from uecraytracing_amd.records import FLAG_COUNT_WORK, FLAG_ONE_LANE, image_height_for, make_params
+
+    spheres, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
+    W = a.width
+    H = image_height_for(W)
+    out = {"workload": f"final42_{W}x{H}x{a.spp}_d50", "calls": []}
+    with yk.Renderer(0) as r:
+        r.set_scene(spheres, cam)
+        imgs = []
+        for flags in (FLAG_COUNT_WORK, FLAG_COUNT_WORK | FLAG_ONE_LANE):
+            imgs.append(r.render(make_params(W, H, a.spp, 50, 404, flags=flags)))
+            st = r.stats()
+            out["calls"].append({"flags": flags, "launches": st["launches"],
+                                 **{k: st[k] for k in ("samples", "segments", "sphere_tests", "sqrt_calls",
+                                                       "newton_calls", "newton_iters", "node_visits",
+                                                       "linear_scans", "mt_fallbacks")},
+                                 "work": st["work"]})
+        out["images_equal"] = bool((imgs[0] == imgs[1]).all())
+    js = json.dumps(out)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(js + "\n")
+    print(js)
+
+
+if __name__ == "__main__":
+    main()

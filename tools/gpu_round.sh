@@ -1,0 +1,10 @@
+# GPU tests then the full measurement set (tools/gpu_profile_all.sh) of the current build.
+# usage: bash tools/gpu_round.sh <tag>   → gpurun_out/<tag>/
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+T=${1:-r02}
+mkdir -p gpurun_out/$T
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/$T/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/$T/gpu_tests.log
+bash tools/gpu_profile_all.sh $T

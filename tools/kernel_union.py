@@ -1,0 +1,43 @@
+"""Per-launch duration of a kernel from a rocprofv3 kernel trace, counting overlap once.
+
+The render launches alternate between two streams and overlap (launch c + 1 starts on the CUs
+launch c's draining blocks free), so rocprofv3's per-dispatch average counts the overlapped time
+twice.  This reports, for the dispatches whose name contains the substring: the plain average
+span (what --stats prints), the UNION of the spans, and union / dispatches — the figure bench.py
+divides by (`roofline.launch_ms`).
+usage: python tools/kernel_union.py <run_kernel_trace.csv> [kernel-substring] [out.json]
+"""
+import csv
+import json
+import sys
+
+
+def main():
+    path = sys.argv[1]
+    kern = sys.argv[2] if len(sys.argv) > 2 else "yk_render_persistent<true, 0>"
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                for r in csv.DictReader(open(path)) if kern in r["Kernel_Name"])
+    if not iv:
+        raise SystemExit(f"no dispatch of {kern!r} in {path}")
+    union = 0
+    cur_s, cur_e = iv[0]
+    for s, e in iv[1:]:
+        if s > cur_e:
+            union += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    union += cur_e - cur_s
+    spans = sum(e - s for s, e in iv)
+    out = {"trace": path, "kernel": kern, "dispatches": len(iv),
+           "avg_span_ms": spans / len(iv) / 1e6, "union_ms": union / 1e6,
+           "union_per_dispatch_ms": union / len(iv) / 1e6,
+           "overlap_fraction_of_spans": 1 - union / spans}
+    js = json.dumps(out, indent=1)
+    if len(sys.argv) > 3:
+        open(sys.argv[3], "w").write(js + "\n")
+    print(js)
+
+
+if __name__ == "__main__":
+    main()

@@ -82,7 +82,7 @@ def load_library():
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
         f.argtypes, f.restype = args, res
-    if lib.ykgpu_abi_version() != 5:
+    if lib.ykgpu_abi_version() != 6:
         raise YkError("ABI version mismatch")
     _lib = lib
     return lib

@@ -5,8 +5,8 @@
 // samples → to_color3b) and the recursion of yk/raytracer.hpp:19-37.
 //
 // Execution model:
-//   * a render call is a few LAUNCHES of K samples per pixel (8, 32, 128, ... up to an 8 GB
-//     colour budget).  Per launch: yk_mt_warmup (x_397 of every sample's mt19937 seeding
+//   * a render call is a sequence of LAUNCHES of K samples per pixel (8, 32, then at most
+//     kLaunchSpp = 64; 1920x1080x512: 8, 32, 7 x 64, 24).  Per launch: yk_mt_warmup (x_397 of every sample's mt19937 seeding
 //     sequence, second stream), yk_render_persistent (the paths), yk_reduce_samples (the
 //     reference's strictly sequential per-pixel sum and to_color3b, third stream).
 //   * yk_render_persistent is one persistent grid over SAMPLE SLOTS: a lane runs one path at a
@@ -90,7 +90,7 @@ using DevNode = ykbvh::WideNode;
 #else
 using DevNode = ykbvh::SlabNode;
 #endif
-constexpr int kCounters = 24;  // [16..18]: timeline, [19..22]: diag (diagnostic builds)
+constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (diagnostic builds), [24..31]: work
 
 // Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
 // points, summed per phase into counters[8..13] (refill, start, traversal, candidates, shade,
@@ -118,6 +118,7 @@ constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
 #define YK_STR2(x) #x
 #define YK_STR(x) YK_STR2(x)
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
+constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 
 struct KernelArgs {
   yk_camera cam;
@@ -426,6 +427,10 @@ void yk_render_persistent(KernelArgs ka) {
     leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
   }
   int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlock]
+  // YK_FLAG_ONE_LANE (counting instance only): lanes 1..63 leave here, after the block's last
+  // barrier, so every wave-instruction below is one lane's (the profiler's per-wave FP64 counters
+  // then count that lane's executed operations exactly: DESIGN.md §5)
+  if (kCount && (ka.flags & kFlagOneLane) && lane != 0) return;
 #if YK_RENDER_PRIO
   // the warm-up waves sharing the SIMDs (priority 0) get only the issue slots the render leaves
   __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);
@@ -436,6 +441,8 @@ void yk_render_persistent(KernelArgs ka) {
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
 
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0, n_ncall = 0, n_nit = 0;
+  uint32_t n_dpos = 0;  // leaf tests with disc >= 0 (their root bounds are computed)
+  uint32_t n_lamb = 0, n_metal = 0, n_fuzz = 0, n_diel = 0;  // hits shaded per material kind
 
 #if YK_ABLATE & 8
   uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -672,6 +679,7 @@ void yk_render_persistent(KernelArgs ka) {
               const double c = ykd::len2(oc) - sg.rr;
               const double disc = hb * hb - a * c;
               if (disc < 0) continue;
+              if (kCount) ++n_dpos;
 #if YK_ABLATE & 8
               ++st_diag0;
 #endif
@@ -782,11 +790,14 @@ void yk_render_persistent(KernelArgs ka) {
         bool scattered = true, push = true;
         v3 nd;
         if (m.kind == YK_MATERIAL_LAMBERTIAN) {  // material.hpp:50-59
+          if (kCount) ++n_lamb;
           nd = ykd::add(nrm, un);
           if (ykd::near_zero(nd)) nd = nrm;
         } else if (m.kind == YK_MATERIAL_METAL) {  // material.hpp:67-75 (+ fuzz extension)
+          if (kCount) ++n_metal;
           nd = ykd::reflect(un, nrm);
           if (m.fuzz > 0) {  // random_in_unit_sphere, material.hpp:27-30
+            if (kCount) ++n_fuzz;
             v3 ru = ykd::random_vec(g, -1, 1);
             ru = ykd::divs_fast(ru, ykd::nsqrt_c(ykd::len2(ru), n_ncall, n_nit));
             const double k = ykd::uniform(g, 0.01, 0.99);
@@ -794,6 +805,7 @@ void yk_render_persistent(KernelArgs ka) {
           }
           scattered = ykd::dot(nd, nrm) > 0;
         } else {  // dielectric extension (attenuation (1,1,1): multiplying by 1.0 is exact)
+          if (kCount) ++n_diel;
           push = false;
           const double ratio = front ? (1.0 / m.ior) : m.ior;
           const v3 unit = un;
@@ -867,6 +879,11 @@ void yk_render_persistent(KernelArgs ka) {
     atomicAdd(&ka.counters[5], (unsigned long long)n_lin);
     atomicAdd(&ka.counters[6], (unsigned long long)n_ncall);
     atomicAdd(&ka.counters[7], (unsigned long long)n_nit);
+    atomicAdd(&ka.counters[24], (unsigned long long)n_dpos);
+    atomicAdd(&ka.counters[25], (unsigned long long)n_lamb);
+    atomicAdd(&ka.counters[26], (unsigned long long)n_metal);
+    atomicAdd(&ka.counters[27], (unsigned long long)n_fuzz);
+    atomicAdd(&ka.counters[28], (unsigned long long)n_diel);
   }
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
@@ -1392,6 +1409,7 @@ constexpr uint64_t kWarmBytes = 8ull << 30;
 #define YK_FIRST_LAUNCH 8
 #endif
 constexpr uint32_t kFirstLaunch = YK_FIRST_LAUNCH;  // samples per pixel in the first launch
+static_assert(YK_FIRST_LAUNCH >= 1 && YK_LAUNCH_SPP >= 1, "launch sizes must be >= 1 sample per pixel");
 #ifndef YK_TILE
 #define YK_TILE 8
 #endif
@@ -1456,12 +1474,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   rc = ensure_order(ctx, p->image_width, p->row_count,
                     p->row_count > 1 && p->row_band_log2 < 3 ? p->row_stride : 1);
   if (rc) return rc;
-  // Launch schedule (samples per pixel per launch): 8, 32, 128, ... growing x4 up to the colour
-  // budget (24 B per sample slot, kColourBytes per launch), the last one taking a small
-  // remainder with it.  The first render waits only for an 8-sample warm-up; every later
-  // warm-up is ~0.15x the render before it, so it finishes underneath; and each launch ends with
-  // the tail of its longest paths (~1 ms), so there are few launches (1920x1080x512: 8, 32, 128,
-  // 172, 172).  Independent of the image size, which matters for the per-rank tiles of N GPUs.
+  // Launch schedule (samples per pixel per launch): 8, 32, then kLaunchSpp (64) per launch, also
+  // capped by the colour budget (24 B per sample slot, kColourBytes per launch); the last launch
+  // takes a small remainder with it (1920x1080x512: 8, 32, 7 x 64, 24 = ten launches).  The first
+  // render waits only for an 8-sample warm-up; every later warm-up is ~0.15x the render before it,
+  // so it finishes underneath.  Each launch ends with the tail of its longest paths (~1 ms), but
+  // launches alternate between two streams, so that drain overlaps the next launch: ten mid-sized
+  // launches beat five large ones.  Independent of the image size, which matters
+  // for the per-rank tiles of N GPUs.
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
   const uint32_t spp = p->samples_per_pixel;
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
@@ -1666,6 +1686,7 @@ int finish_stats(ykgpu_context* ctx) {
   for (int k = 0; k < 8; ++k) ctx->stats.phase_cycles[k] = c[8 + k];
   for (int k = 0; k < 3; ++k) ctx->stats.timeline[k] = c[16 + k];
   for (int k = 0; k < 4; ++k) ctx->stats.diag[k] = c[19 + k];
+  for (int k = 0; k < 8; ++k) ctx->stats.work[k] = c[24 + k];
   ctx->stats.total_ms = ms;
   double tw = 0, tr = 0, tp = 0, busy = 0;
   for (uint32_t k = 0; k + 5 < ctx->lev_used; k += 6) {
@@ -1860,7 +1881,9 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
     mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0u, 0ull};
   }
   YK_HIP(hipSetDevice(ctx->device));
-  YK_HIP(hipStreamSynchronize(ctx->stream));
+  // a render enqueued by ykgpu_render_async on the caller's stream (and its launches on the
+  // context's own streams) may still read the scene: wait for the whole device
+  YK_HIP(hipDeviceSynchronize());
   if (count > ctx->nspheres || !ctx->d_geo) {
     (void)hipFree(ctx->d_geo);
     (void)hipFree(ctx->d_mat);

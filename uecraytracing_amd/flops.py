@@ -1,0 +1,90 @@
+"""FP64 flop models of the render kernel (yk_render_persistent), DESIGN.md §5.
+
+Two models over the kernel's own work counters (a YK_FLAG_COUNT_WORK launch, `Renderer.stats()`):
+
+* ALGORITHMIC — the flops of the reference's own expressions for the work the kernel did
+  (sphere.hpp:25-48, math.hpp:10-19, material.hpp, camera.hpp, raytracer.hpp), one flop per
+  IEEE add / mul / divide.  This is the roofline's numerator (bench.py `roofline`).
+* IMPLEMENTATION — the FP64 operations the gfx950 kernel actually issues for the same work,
+  weighted as the hardware counter SQ_INSTS_VALU_FLOPS_FP64 weighs them (v_add/v_mul/
+  v_rcp/v_rsq_f64 = 1, v_fma/v_div_fmas_f64 = 2; v_cmp/v_max/v_cvt/v_ldexp/v_div_scale/
+  v_div_fixup_f64 = 0 — calibrated on tools/flopcal.hip, profiles/r02_fp64_reconcile.json).
+  A division is the refined-reciprocal sequence (rcp + 4 FMA) plus mul + 2 FMA; math::sqrt
+  starts at a refined rsq and iterates divisions; the BVH's root bounds add work the reference
+  does not have.  Per-unit weights are read off the compiled sequences (yk_device.hpp functions
+  compiled alone and counted in the ISA, tools/fp64_reconcile_summary.py).
+
+The counter counts once per WAVE-instruction whatever the exec mask: a launch with all lanes
+active reports issued lane-slots / 64; a YK_FLAG_ONE_LANE launch reports exactly the operations
+its lanes executed, which is what the implementation model predicts.
+"""
+from __future__ import annotations
+
+# --- algorithmic (reference expressions) -------------------------------------------------
+ALG_PER_SPHERE_TEST = 17  # sphere.hpp:29-33: oc (3), dot (5), len2 - r^2 (6), hb^2 - a*c (3)
+ALG_PER_ROOT = 4          # sphere.hpp:36-39: (-hb -/+ sq) / a, one or two roots
+ALG_PER_NEWTON_CALL = 1   # math.hpp:12: x = s / 2
+ALG_PER_NEWTON_ITER = 3   # math.hpp:14-17: s/x, x + ., ./2
+ALG_PER_SEGMENT = 40      # |d|^2, hit record (p, normal, face: 17), normalize (8), scatter (~10)
+ALG_PER_SAMPLE = 30       # jitter + camera ray (24), accumulate + attenuation products (~6)
+
+
+def algorithmic(st: dict) -> float:
+    """FP64 flops of the reference's arithmetic for the counted work (per call)."""
+    return (st["sphere_tests"] * ALG_PER_SPHERE_TEST + st["sqrt_calls"] * ALG_PER_ROOT
+            + st["newton_calls"] * ALG_PER_NEWTON_CALL + st["newton_iters"] * ALG_PER_NEWTON_ITER
+            + st["segments"] * ALG_PER_SEGMENT + st["samples"] * ALG_PER_SAMPLE)
+
+
+def algorithmic_terms() -> str:
+    return (f"{ALG_PER_SPHERE_TEST}/sphere test + {ALG_PER_ROOT}/exact root + math::sqrt "
+            f"({ALG_PER_NEWTON_CALL}/call + {ALG_PER_NEWTON_ITER}/iteration) + {ALG_PER_SEGMENT}/segment "
+            f"+ {ALG_PER_SAMPLE}/sample")
+
+
+# --- implementation (counter-weighted FP64 operations the kernel issues per lane) ----------
+IMPL = {
+    # leaf: the reference's discriminant (9 add + 8 mul, no contraction)
+    "sphere_test": 17,
+    # disc >= 0: sqrt_bound (rsq + 2 mul + 2 fma = 7), two roots x 1/a (4), margin (4),
+    # r2 + m, r1 - m, and the upper bound (2)
+    "leaf_disc_pos": 19,
+    # exact candidate: discriminant again (17) + (-hb - sq) + div_by (mul + 2 fma = 5); the
+    # second root (another 6) when the first is below t_min is folded into the 1.1 factor
+    "candidate": 17 + 6 * 1.1,
+    "newton_call": 17,   # sqrt_start: rsq, 2 mul, 7 fma
+    "newton_iter": 16,   # rcp_refined (rcp + 4 fma = 9) + div_pos (5) + add + mul 0.5
+    # every segment: a = len2(d) (5) + rcp_bound (rcp + 2 fma = 5); the shading length (len2 5)
+    # and divs_fast (rcp_refined 9 + 3 x div_by 5 = 24) of the one shared normalisation
+    "segment": 10 + 29,
+    # a hit: p = o + d T (6), p - c (3), divs_fast by the radius (24), dot(d, n) (5)
+    "hit": 38,
+    "lambertian": 9 + 3,          # random_vec (3 x 3 adds; the powers of two are v_ldexp) + add
+    "metal": 12 + 5,              # reflect (6 mul + 6 add) + dot(nd, n)
+    # fuzz: random_vec (9) + len2 (5) + divs_fast (24) + uniform (3) + 2 scalings (6) + add (3)
+    "metal_fuzz": 50,
+    # dielectric (yk_device.hpp reflectance etc.): half the hits divide 1/ior (14); dot, 1-ct^2,
+    # ratio*sn (8); Schlick (25); uniform (2); reflect (12) or refract (21): ~58
+    "dielectric": 58,
+    "sky": 8,                     # (y + 1)/2 and the lerp (5 add + 3 mul)
+    "attenuation": 3,             # unwinding: 3 mul per scattering sphere on the stack
+    # sample start: 2 uniform(0,1) (2 each) + 2 Markstein quotients (add + mul + 2 fma = 6 each)
+    # + camera ray (5 x 3)
+    "sample": 31,
+    "candidate_rcp": 9,           # rcp_refined(a), once per segment with candidates (~ hits)
+}
+
+
+def implementation(st: dict) -> float:
+    """Counter-weighted FP64 operations the kernel executes for the counted work (per call)."""
+    w = st["work"]
+    dpos, lamb, metal, fuzz, diel = w[0], w[1], w[2], w[3], w[4]
+    hits = lamb + metal + diel
+    sky = st["segments"] - hits  # every other segment that ran shading ended in the sky
+    return (st["sphere_tests"] * IMPL["sphere_test"] + dpos * IMPL["leaf_disc_pos"]
+            + st["sqrt_calls"] * IMPL["candidate"] + hits * IMPL["candidate_rcp"]
+            + st["newton_calls"] * IMPL["newton_call"] + st["newton_iters"] * IMPL["newton_iter"]
+            + st["segments"] * IMPL["segment"] + hits * IMPL["hit"]
+            + lamb * IMPL["lambertian"] + metal * IMPL["metal"] + fuzz * IMPL["metal_fuzz"]
+            + diel * IMPL["dielectric"] + sky * IMPL["sky"] + (lamb + metal) * IMPL["attenuation"]
+            + st["samples"] * IMPL["sample"])

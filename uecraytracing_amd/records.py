@@ -20,6 +20,7 @@ SEED_COUNTER = 0
 SEED_RANDOM_DEVICE = 1
 FLAG_COUNT_WORK = 1
 FLAG_LINEAR_SCAN = 2
+FLAG_ONE_LANE = 4
 
 YK_OK = 0
 ERRORS = {
@@ -110,6 +111,7 @@ class RenderStats(ctypes.Structure):
         ("launches", ctypes.c_uint32),
         ("grid_blocks", ctypes.c_uint32),
         ("render_busy_ms", ctypes.c_double),
+        ("work", ctypes.c_uint64 * 8),
     ]
 
     def as_dict(self):
@@ -117,6 +119,7 @@ class RenderStats(ctypes.Structure):
         d["phase_cycles"] = list(self.phase_cycles)
         d["timeline"] = list(self.timeline)
         d["diag"] = list(self.diag)
+        d["work"] = list(self.work)
         return d
 
 
