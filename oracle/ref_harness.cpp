@@ -27,6 +27,8 @@
 //   render32 / samples32: the same with T = float (render<float>(); radius literals as T(...))
 //   render_x128 / samples_x128 / render32_x128 / samples32_x128: the engine is the reference's
 //     yk::xor128 (random.hpp:18-41) seeded with the same per-sample counter, in place of mt19937
+//   render_file / samples_file (and the 32 / _x128 forms): <scene> is a scene file of 5, 24 or 48
+//     spheres (configs 2-5 content: dielectric, fuzzed metal, thin-lens camera; see below)
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -116,26 +118,200 @@ struct job {
   std::uint32_t W, H, spp, depth, seed0;
 };
 
+// ---- BASELINE configs 2-5 content through the reference's own integrator ---------------------
+// The reference has no dielectric, no fuzzed metal and no positionable camera, but
+// its integrator takes any material type: concepts::material is `true` (material.hpp:22-23),
+// hittable_list::scatter dispatches by rec.id (hittable_list.hpp:60-73) to sphere::scatter_impl
+// (sphere.hpp:50-54), which calls the material, and ray_color multiplies and recurses
+// (raytracer.hpp:19-37).  The three extension bodies below are OURS — they restate
+// oracle/yk_oracle_path.h and the kernel — and everything around them is the reference's code:
+// ray_color, the ordered closest-hit fold, sphere::hit_impl, set_face_normal, mt19937,
+// uniform_real_distribution, math::sqrt, reflect, normalized and random_in_unit_sphere.  A golden
+// rendered here therefore pins the extensions' RNG interleaving and their integration to the
+// reference; only the scatter bodies and the camera's lens remain unpinned.
+
+// fuzzed metal: metal::scatter (material.hpp:67-75) with RTIOW's `reflected + fuzz *
+// random_in_unit_sphere()` — the reference's own random_in_unit_sphere (material.hpp:27-30), whose
+// two operands g++ (the reference's compiler, Makefile:1) evaluates right to left: the length
+// factor uniform(0.01, 0.99) is drawn BEFORE the vector.
+template <class U>
+struct fuzzy_metal {
+  yk::color3<U> albedo;
+  double fuzz;
+  template <class T, class Gen>
+  constexpr std::optional<std::pair<yk::color3<U>, yk::ray<T>>> scatter(const yk::ray<T>& r_in,
+                                                                        const yk::hit_record<T>& rec,
+                                                                        Gen& gen) const {
+    auto reflected = reflect(r_in.direction.normalized(), rec.normal);
+    reflected = reflected + T(fuzz) * yk::random_in_unit_sphere<T>(gen);
+    auto scattered = yk::ray(rec.p, reflected);
+    if (dot(scattered.direction, rec.normal) > 0) return std::make_pair(albedo, scattered);
+    return std::nullopt;
+  }
+};
+
+// dielectric (RTIOW): Snell with total internal reflection, Schlick's reflectance, attenuation 1
+template <class U>
+struct dielectric_ext {
+  double ior;
+  template <class T>
+  static constexpr T reflectance(T cosine, T ref_idx) {
+    T r0 = (T(1) - ref_idx) / (T(1) + ref_idx);
+    r0 = r0 * r0;
+    T x = T(1) - cosine;
+    return r0 + (T(1) - r0) * ((((x * x) * x) * x) * x);
+  }
+  template <class T, class Gen>
+  constexpr std::optional<std::pair<yk::color3<U>, yk::ray<T>>> scatter(const yk::ray<T>& r_in,
+                                                                        const yk::hit_record<T>& rec,
+                                                                        Gen& gen) const {
+    const T ir = T(ior);
+    const T ratio = rec.front_face ? (T(1) / ir) : ir;
+    const auto unit = r_in.direction.normalized();
+    T ct = dot(-unit, rec.normal);
+    if (!(ct < T(1))) ct = T(1);
+    const T st = yk::math::sqrt(T(1) - ct * ct);
+    const bool cannot = ratio * st > T(1);
+    yk::vec3<T> dir;
+    if (cannot || reflectance(ct, ratio) > yk::uniform_real_distribution<T>(0, 1)(gen)) {
+      dir = reflect(unit, rec.normal);
+    } else {
+      const auto perp = (unit + ct * rec.normal) * ratio;
+      const T pl = T(1) - perp.length_squared();
+      dir = perp + rec.normal * (-yk::math::sqrt(pl < 0 ? -pl : pl));
+    }
+    return std::make_pair(yk::color3<U>(1.0, 1.0, 1.0), yk::ray(rec.p, dir));
+  }
+};
+
+// one material type for every sphere of a scene file: dispatches to the reference's lambertian
+// and metal (fuzz 0) or to the extensions above
+struct any_material {
+  std::uint32_t kind;  // 0 lambertian, 1 metal, 2 dielectric (include/ykgpu.h YK_MATERIAL_*)
+  yk::color3<double> albedo;
+  double fuzz, ior;
+  template <class T, class Gen>
+  constexpr std::optional<std::pair<yk::color3<double>, yk::ray<T>>> scatter(const yk::ray<T>& r,
+                                                                             const yk::hit_record<T>& rec,
+                                                                             Gen& gen) const {
+    if (kind == 0) return yk::lambertian<double>(albedo).scatter(r, rec, gen);
+    if (kind == 1) {
+      if (fuzz > 0) return fuzzy_metal<double>{albedo, fuzz}.scatter(r, rec, gen);
+      return yk::metal<double>(albedo).scatter(r, rec, gen);
+    }
+    return dielectric_ext<double>{ior}.scatter(r, rec, gen);
+  }
+};
+
+// positionable thin-lens camera (RTIOW): the reference camera's get_ray (camera.hpp:29-32) as
+// llc + u*horizontal + v*vertical - origin, the origin moved by a point of the lens disk drawn by
+// rejection (x, then y, each uniform(-1, 1))
+template <class T>
+struct lens_camera {
+  yk::vec3<T> origin, lower_left_corner, horizontal, vertical, lens_u, lens_v;
+  T lens_radius;
+  template <class Gen>
+  constexpr yk::ray<T> get_ray(T u, T v, Gen& gen) const {
+    auto org = origin;
+    auto dir = lower_left_corner + u * horizontal + v * vertical - origin;
+    if (lens_radius > 0) {
+      T px, py;
+      for (;;) {
+        px = yk::uniform_real_distribution<T>(-1, 1)(gen);
+        py = yk::uniform_real_distribution<T>(-1, 1)(gen);
+        if (px * px + py * py < T(1)) break;
+      }
+      const T rx = px * lens_radius, ry = py * lens_radius;
+      const auto off = lens_u * rx + lens_v * ry;
+      org = org + off;
+      dir = dir - off;
+    }
+    return yk::ray<T>{P<T>(org.x, org.y, org.z), dir};
+  }
+};
+
+// scene files (include/ykgpu.h yk_scene_write: "yk-scene 1", one camera line, sphere lines)
+struct file_sphere {
+  double c[3], r, albedo[3], fuzz, ior;
+  std::uint32_t kind;
+};
+struct scene_file {
+  double cam[19];
+  std::vector<file_sphere> s;
+};
+bool read_scene_file(const char* path, scene_file& out) {
+  FILE* f = std::fopen(path, "r");
+  if (!f) return false;
+  char line[2048];
+  bool cam = false;
+  while (std::fgets(line, sizeof line, f)) {
+    if (!std::strncmp(line, "camera", 6)) {
+      const char* p = line + 6;
+      for (int k = 0; k < 19; ++k) {
+        char* e = nullptr;
+        out.cam[k] = std::strtod(p, &e);
+        p = e;
+      }
+      cam = true;
+    } else if (!std::strncmp(line, "sphere", 6)) {
+      file_sphere s{};
+      char kind[32] = {0};
+      if (std::sscanf(line + 6, "%31s %lf %lf %lf %lf %lf %lf %lf %lf %lf", kind, &s.c[0], &s.c[1], &s.c[2], &s.r,
+                      &s.albedo[0], &s.albedo[1], &s.albedo[2], &s.fuzz, &s.ior) != 10)
+        return false;
+      s.kind = !std::strcmp(kind, "lambertian") ? 0u : !std::strcmp(kind, "metal") ? 1u : 2u;
+      out.s.push_back(s);
+    }
+  }
+  std::fclose(f);
+  return cam;
+}
+template <class T>
+lens_camera<T> file_camera(const scene_file& sf) {
+  auto v = [&](int k) { return yk::vec3<T>{T(sf.cam[k]), T(sf.cam[k + 1]), T(sf.cam[k + 2])}; };
+  return {v(0), v(3), v(6), v(9), v(12), v(15), T(sf.cam[18])};
+}
+template <class T, std::size_t I>
+using file_sphere_t = yk::sphere<T, any_material>;
+template <class T>
+file_sphere_t<T, 0> make_sphere(const file_sphere& s) {
+  return yk::sphere(P<T>(s.c[0], s.c[1], s.c[2]), T(s.r),
+                    any_material{s.kind, {s.albedo[0], s.albedo[1], s.albedo[2]}, s.fuzz, s.ior});
+}
+// a compile-time tuple of N spheres filled from the file (the tuple API needs N at compile time)
+template <class T, std::size_t... I>
+auto file_world(const scene_file& sf, std::index_sequence<I...>) {
+  return yk::hittable_list<T, file_sphere_t<T, I>...>(std::tuple<file_sphere_t<T, I>...>(make_sphere<T>(sf.s[I])...));
+}
+
 // T = double is render() as shipped (source.cpp:98); T = float is render<float>(): geometry,
 // camera, canonicals (one draw each) and math::sqrt in float, colour still double
 // (raytracer<T, double>, lambertian<double>).
-template <class T, class E, class World>
-yk::color3d sample_color(const World& world, const job& j, std::uint32_t y, std::uint32_t x,
+// camera<T>::get_ray(u, v) (camera.hpp:29-32), or the lens camera's, which also draws
+template <class T, class Cam, class Gen>
+yk::ray<T> camera_ray(const Cam& cam, T u, T v, Gen& gen) {
+  if constexpr (requires { cam.get_ray(u, v, gen); })
+    return cam.get_ray(u, v, gen);
+  else
+    return cam.get_ray(u, v);
+}
+
+template <class T, class E, class World, class Cam>
+yk::color3d sample_color(const World& world, const Cam& cam, const job& j, std::uint32_t y, std::uint32_t x,
                          std::uint32_t s, std::uint64_t* draws) {
   const yk::raytracer<T, double> tracer = {};
-  const yk::camera<T> cam = {};
   E g(j.seed0 + (y * j.W + x) * j.spp + s);
   counting_gen<E> gen{&g};
   yk::uniform_real_distribution<T> dist(0, 1);
-  auto u = (x + dist(gen)) / j.W;
-  auto v = (j.H - y - 1 + dist(gen)) / j.H;
-  auto c = tracer.ray_color(cam.get_ray(u, v), world, j.depth, gen);
+  T u = (x + dist(gen)) / j.W;
+  T v = (j.H - y - 1 + dist(gen)) / j.H;
+  auto c = tracer.ray_color(camera_ray<T>(cam, u, v, gen), world, j.depth, gen);
   if (draws) *draws = gen.n;
   return c;
 }
 
-template <class T, class E, class World>
-int render(const World& world, const job& j, const char* out_rgb, const char* out_sums) {
+template <class T, class E, class World, class Cam>
+int render(const World& world, const Cam& cam, const job& j, const char* out_rgb, const char* out_sums) {
   std::vector<unsigned char> rgb(std::size_t(j.W) * j.H * 3);
   std::vector<double> sums(std::size_t(j.W) * j.H * 3);
   for (std::uint32_t y = 0; y < j.H; ++y) {
@@ -143,7 +319,7 @@ int render(const World& world, const job& j, const char* out_rgb, const char* ou
       auto iota = std::views::iota(0u, j.spp);
       yk::color3d pc = std::transform_reduce(
           iota.begin(), iota.end(), yk::color3d(0, 0, 0), std::plus{},
-          [&](auto s) { return sample_color<T, E>(world, j, y, x, s, nullptr); });
+          [&](auto s) { return sample_color<T, E>(world, cam, j, y, x, s, nullptr); });
       const std::size_t i = std::size_t(y) * j.W + x;
       sums[3 * i + 0] = pc.r;
       sums[3 * i + 1] = pc.g;
@@ -170,15 +346,15 @@ int render(const World& world, const job& j, const char* out_rgb, const char* ou
   return 0;
 }
 
-template <class T, class E, class World>
-int samples(const World& world, const job& j, int argc, char** argv) {
+template <class T, class E, class World, class Cam>
+int samples(const World& world, const Cam& cam, const job& j, int argc, char** argv) {
   std::printf("[\n");
   for (int k = 0; k + 2 < argc; k += 3) {
     std::uint32_t y = std::strtoul(argv[k], nullptr, 10);
     std::uint32_t x = std::strtoul(argv[k + 1], nullptr, 10);
     std::uint32_t s = std::strtoul(argv[k + 2], nullptr, 10);
     std::uint64_t n = 0;
-    auto c = sample_color<T, E>(world, j, y, x, s, &n);
+    auto c = sample_color<T, E>(world, cam, j, y, x, s, &n);
     std::printf("  {\"y\": %u, \"x\": %u, \"s\": %u, \"draws\": %llu, \"rgb\": [\"%a\", \"%a\", \"%a\"]}%s\n",
                 y, x, s, (unsigned long long)n, c.r, c.g, c.b, (k + 5 < argc) ? "," : "");
   }
@@ -266,14 +442,37 @@ int kat() {
   return 0;
 }
 
-template <class T, class E, class World>
-int dispatch_world(const World& w, const char* mode, const job& j, int argc, char** argv) {
-  if (!std::strncmp(mode, "render", 6)) return render<T, E>(w, j, argv[0], argc > 1 ? argv[1] : nullptr);
-  return samples<T, E>(w, j, argc, argv);
+template <class T, class E, class World, class Cam = yk::camera<T>>
+int dispatch_world(const World& w, const char* mode, const job& j, int argc, char** argv, const Cam& cam = {}) {
+  if (!std::strncmp(mode, "render", 6)) return render<T, E>(w, cam, j, argv[0], argc > 1 ? argv[1] : nullptr);
+  return samples<T, E>(w, cam, j, argc, argv);
+}
+
+// a scene file (configs 2-5 content): N spheres in a compile-time tuple, the lens camera
+template <class T, class E, std::size_t N>
+int dispatch_file_n(const scene_file& sf, const char* mode, const job& j, int argc, char** argv) {
+  return dispatch_world<T, E>(file_world<T>(sf, std::make_index_sequence<N>{}), mode, j, argc, argv,
+                              file_camera<T>(sf));
+}
+template <class T, class E>
+int dispatch_file(const std::string& path, const char* mode, const job& j, int argc, char** argv) {
+  scene_file sf;
+  if (!read_scene_file(path.c_str(), sf)) {
+    std::fprintf(stderr, "cannot read scene file %s\n", path.c_str());
+    return 2;
+  }
+  switch (sf.s.size()) {
+    case 5: return dispatch_file_n<T, E, 5>(sf, mode, j, argc, argv);
+    case 24: return dispatch_file_n<T, E, 24>(sf, mode, j, argc, argv);
+    case 48: return dispatch_file_n<T, E, 48>(sf, mode, j, argc, argv);
+  }
+  std::fprintf(stderr, "scene files of 5, 24 or 48 spheres only (tuple sizes compiled in), got %zu\n", sf.s.size());
+  return 2;
 }
 
 template <class T, class E>
 int dispatch(const std::string& scene, const char* mode, const job& j, int argc, char** argv) {
+  if (std::strstr(mode, "_file")) return dispatch_file<T, E>(scene, mode, j, argc, argv);
   if (scene == "ref4") return dispatch_world<T, E>(scene_ref4<T>(), mode, j, argc, argv);
   if (scene == "lambert3") return dispatch_world<T, E>(scene_lambert3<T>(), mode, j, argc, argv);
   if (scene == "mixed12") return dispatch_world<T, E>(scene_mixed12<T>(), mode, j, argc, argv);

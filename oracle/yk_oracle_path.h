@@ -149,10 +149,13 @@ static int SFX(scatter)(const yk_sphere* sp, V3 rd, const HIT* rec, mt_t* g, c3*
     }
     case YK_MATERIAL_METAL: { /* material.hpp:67-75 (+ fuzz extension) */
       V3 refl = SFX(v3_reflect)(SFX(v3_normalized)(rd), rec->normal);
-      if (sp->fuzz > 0) { /* extension: random_in_unit_sphere, material.hpp:27-30 */
+      if (sp->fuzz > 0) { /* extension: + fuzz * random_in_unit_sphere (material.hpp:27-30) */
+        /* the reference's random_in_unit_sphere returns random(-1,1).normalize() * uniform(0.01,
+         * 0.99); g++ (its compiler, Makefile:1) evaluates that product's operands right to left,
+         * so the length factor is drawn BEFORE the vector (pinned by the harness goldens) */
+        R k = SFX(uniform)(g, (R)0.01, (R)0.99);
         V3 ru = SFX(v3_random)(g, -1, 1);
         ru = SFX(v3_div)(ru, SFX(nsqrt)(SFX(v3_len2)(ru)));
-        R k = SFX(uniform)(g, (R)0.01, (R)0.99);
         refl = SFX(v3_add)(refl, SFX(v3_mul)(SFX(v3_mul)(ru, k), (R)sp->fuzz));
       }
       if (SFX(v3_dot)(refl, rec->normal) > 0) {

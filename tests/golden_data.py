@@ -30,6 +30,36 @@ def sums(entry):
     return np.frombuffer(b, "<f8").reshape(entry["H"], entry["W"], 3)
 
 
+def read_scene_file(path):
+    """Pure-Python reader of the scene-file format (include/ykgpu.h yk_scene_write): the fixtures'
+    configs 2-5 scenes, read without the product library.  Returns (spheres, Camera)."""
+    from uecraytracing_amd.records import (Camera, D3, MATERIAL_DIELECTRIC, MATERIAL_LAMBERTIAN,
+                                           MATERIAL_METAL, Sphere)
+    kinds = {"lambertian": MATERIAL_LAMBERTIAN, "metal": MATERIAL_METAL, "dielectric": MATERIAL_DIELECTRIC}
+    cam, sph = None, []
+    for line in open(path):
+        f = line.split()
+        if not f or f[0].startswith("#") or f[0] == "yk-scene":
+            continue
+        if f[0] == "camera":
+            v = [float(t) for t in f[1:20]]
+            cam = Camera(*(D3(*v[3 * k:3 * k + 3]) for k in range(6)), v[18])
+        elif f[0] == "sphere":
+            v = [float(t) for t in f[2:11]]
+            sph.append(Sphere(D3(*v[0:3]), v[3], D3(*v[4:7]), v[7], v[8], kinds[f[1]], 0))
+    assert cam is not None, path
+    return sph, cam
+
+
+def scene(entry):
+    """(spheres, camera) of a fixture: a scene file of tests/golden/ (configs 2-5 content, rendered
+    through the reference's integrator with the extension materials) or a named reference scene."""
+    import refscenes
+    if "scene_file" in entry:
+        return read_scene_file(os.path.join(GOLDEN, entry["scene_file"]))
+    return refscenes.SCENES[entry["scene"]](), refscenes.reference_camera()
+
+
 def sha(arr) -> str:
     return hashlib.sha256(np.ascontiguousarray(arr).tobytes()).hexdigest()
 

@@ -30,8 +30,8 @@ def ren():
 
 @pytest.mark.parametrize("entry", MAN["cases"], ids=[c["name"] for c in MAN["cases"]])
 def test_golden_case(ren, entry):
-    sph = refscenes.SCENES[entry["scene"]]()
-    ren.set_scene(sph, refscenes.reference_camera())
+    sph, cam = golden_data.scene(entry)  # scene files: configs 2-5 content (gen_golden.py CASES_FILE)
+    ren.set_scene(sph, cam)
     # fp32 fixtures: the reference's render<float> (YK_PRECISION_FP32); xor128 fixtures: the
     # reference's yk::xor128 as the per-sample engine (YK_RNG_XOR128)
     p = make_params(entry["W"], entry["H"], entry["spp"], entry["depth"], entry["seed0"],

@@ -126,10 +126,12 @@ def test_render_matches_reference_large(entry):
 
 
 def _check_case(entry):
-    sph = refscenes.SCENES[entry["scene"]]()
+    # scene-file cases: configs 2-5 content rendered through the reference's integrator with the
+    # extension materials plugged in (oracle/ref_harness.cpp *_file modes)
+    sph, cam = golden_data.scene(entry)
     p = make_params(entry["W"], entry["H"], entry["spp"], entry["depth"], entry["seed0"],
                     precision=_precision(entry), rng=_rng(entry))
-    rgb, sums, _, _ = oracle_lib.render(sph, refscenes.reference_camera(), p, want_sums=True)
+    rgb, sums, _, _ = oracle_lib.render(sph, cam, p, want_sums=True)
     np.testing.assert_array_equal(rgb, golden_data.rgb(entry))
     assert golden_data.sha(sums) == entry["sums_sha256"]
     ref_sums = golden_data.sums(entry)
@@ -140,7 +142,7 @@ def _check_case(entry):
 @pytest.mark.parametrize("scene", sorted(MAN["samples"]))
 def test_per_sample_paths(scene):
     spec = MAN["samples"][scene]
-    sph, cam = refscenes.SCENES[spec.get("scene") or scene.split("_")[0]](), refscenes.reference_camera()
+    sph, cam = golden_data.scene({"scene": spec.get("scene") or scene.split("_")[0], **spec})
     p = make_params(spec["W"], spec["H"], spec["spp"], spec["depth"], spec["seed0"],
                     precision=_precision(spec), rng=_rng(spec))
     for pt in spec["points"]:

@@ -796,11 +796,14 @@ void yk_render_persistent(KernelArgs ka) {
         } else if (m.kind == YK_MATERIAL_METAL) {  // material.hpp:67-75 (+ fuzz extension)
           if (kCount) ++n_metal;
           nd = ykd::reflect(un, nrm);
-          if (m.fuzz > 0) {  // random_in_unit_sphere, material.hpp:27-30
+          if (m.fuzz > 0) {  // + fuzz * random_in_unit_sphere (material.hpp:27-30)
             if (kCount) ++n_fuzz;
+            // random(-1,1).normalize() * uniform(0.01,0.99): g++, the reference's compiler,
+            // evaluates the product's operands right to left, so the length factor is drawn
+            // first (pinned by the reference-harness goldens, tests/golden/gen_golden.py)
+            const double k = ykd::uniform(g, 0.01, 0.99);
             v3 ru = ykd::random_vec(g, -1, 1);
             ru = ykd::divs_fast(ru, ykd::nsqrt_c(ykd::len2(ru), n_ncall, n_nit));
-            const double k = ykd::uniform(g, 0.01, 0.99);
             nd = ykd::add(nd, ykd::mul(ykd::mul(ru, k), m.fuzz));
           }
           scattered = ykd::dot(nd, nrm) > 0;
@@ -1179,10 +1182,10 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
           if (ykf::near_zero(nd)) nd = nrm;
         } else if (m.kind == YK_MATERIAL_METAL) {
           nd = ykf::reflect(un, nrm);
-          if (m.fuzz > 0) {
+          if (m.fuzz > 0) {  // the length factor first, as in FP64
+            const float k = ykf::uniform(g, 0.01f, 0.99f);
             ykf::v3 ru = ykf::random_vec(g, -1.0f, 1.0f);
             ru = ykf::divs(ru, ykf::nsqrt(ykf::len2(ru), n_nit));
-            const float k = ykf::uniform(g, 0.01f, 0.99f);
             nd = ykf::add(nd, ykf::mul(ykf::mul(ru, k), (float)m.fuzz));
           }
           scattered = ykf::dot(nd, nrm) > 0;
