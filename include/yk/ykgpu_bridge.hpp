@@ -13,8 +13,12 @@
 // the image_t bytes (source.cpp:70-71: row-major, row 0 at the top, RGB interleaved).
 #pragma once
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <iomanip>
+#include <ostream>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -180,6 +184,14 @@ class renderer {
 
   std::vector<uint8_t> render(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
                               uint32_t seed0, const render_options& o) {
+    const yk_render_params p = params(width, height, spp, max_depth, seed0, o);
+    std::vector<uint8_t> img((size_t)width * height * 3);
+    check(ykgpu_render(ctx_, &p, img.data()), "ykgpu_render");
+    return img;
+  }
+
+  static yk_render_params params(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
+                                 uint32_t seed0, const render_options& o) {
     yk_render_params p;
     std::memset(&p, 0, sizeof p);
     p.image_width = width;
@@ -195,9 +207,60 @@ class renderer {
     p.seed_mode = o.seed_mode;
     p.seed_key = o.seed_key;
     p.t_min = o.t_min;
-    std::vector<uint8_t> img((size_t)width * height * 3);
-    check(ykgpu_render(ctx_, &p, img.data()), "ykgpu_render");
-    return img;
+    return p;
+  }
+
+  // ray_color's rays (verbose level 3) of every sample of `rows` image rows from row_begin:
+  // rays[(i*max_rays + k)*6 + {0..5}] = origin xyz, direction xyz of call k of sample
+  // i = (row*W + x)*spp + s; counts[i] = its number of ray_color calls (include/ykgpu.h)
+  void trace(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth, uint32_t seed0,
+             uint32_t row_begin, uint32_t rows, uint32_t max_rays, std::vector<double>& rays,
+             std::vector<uint32_t>& counts, const render_options& o = {}) {
+    yk_render_params p = params(width, height, spp, max_depth, seed0, o);
+    p.row_begin = row_begin;
+    p.row_count = rows;
+    const size_t n = (size_t)rows * width * spp;
+    rays.assign(n * max_rays * 6, 0.0);
+    counts.assign(n, 0);
+    check(ykgpu_render_trace(ctx_, &p, max_rays, rays.data(), counts.data()), "ykgpu_render_trace");
+  }
+
+  // The console output of render()'s loop for the image just rendered, in the reference's order:
+  // "(row,col)" per pixel at verbose >= 1 (source.cpp:128-135), "(row,col,sam)" per sample at
+  // verbose >= 2 (:140-152) and, at verbose > 2, each ray ray_color is called with
+  // (raytracer.hpp:21-25), the ray at depth 0 included.  The reference prints them while it
+  // renders; here they follow the device's render.
+  void print_verbose(std::ostream& os, uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
+                     uint32_t seed0, uint32_t verbose, const render_options& o = {}) {
+    if (!verbose) return;
+    const auto w = [](uint32_t n) { return (int)(std::ceil(std::log10(n)) - 1); };
+    const uint32_t max_rays = max_depth + 1;
+    // row bands of at most ~256 MB of rays
+    const size_t per_row = (size_t)width * spp * max_rays * 6 * sizeof(double);
+    const uint32_t band = verbose > 2 ? (uint32_t)std::max<size_t>(1, (256u << 20) / std::max<size_t>(1, per_row)) : height;
+    std::vector<double> rays;
+    std::vector<uint32_t> counts;
+    for (uint32_t y0 = 0; y0 < height; y0 += band) {
+      const uint32_t rows = std::min(band, height - y0);
+      if (verbose > 2) trace(width, height, spp, max_depth, seed0, y0, rows, max_rays, rays, counts, o);
+      for (uint32_t y = y0; y < y0 + rows; ++y)
+        for (uint32_t x = 0; x < width; ++x) {
+          os << "(row,col) : " << '(' << std::setw(w(height)) << y << ',' << std::setw(w(width)) << x << ')'
+             << std::endl;
+          if (verbose < 2) continue;
+          for (uint32_t s = 0; s < spp; ++s) {
+            os << "(row,col,sam) : " << '(' << std::setw(w(height)) << y << ',' << std::setw(w(width)) << x << ','
+               << std::setw(w(spp)) << s << ')' << std::endl;
+            if (verbose < 3) continue;
+            const size_t i = ((size_t)(y - y0) * width + x) * spp + s;
+            for (uint32_t k = 0; k < counts[i] && k < max_rays; ++k) {
+              const double* r = &rays[(i * max_rays + k) * 6];
+              os << "ray { origin : (" << r[0] << ", " << r[1] << ", " << r[2] << "), direction : (" << r[3]
+                 << ", " << r[4] << ", " << r[5] << ") }" << '\n';
+            }
+          }
+        }
+    }
   }
 
   yk_render_stats stats() {

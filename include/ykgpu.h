@@ -35,11 +35,14 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 6u
+#define YKGPU_ABI_VERSION 7u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
- * METAL with fuzz > 0 and DIELECTRIC are extensions needed by BASELINE configs 2-5 (no
- * reference oracle exists for them: parity unpinned). */
+ * METAL with fuzz > 0 (reflected + fuzz * the reference's random_in_unit_sphere,
+ * material.hpp:27-30) and DIELECTRIC are extensions needed by BASELINE configs 2-5.  The
+ * reference has no code for them, but its integrator takes them: their images are pinned by
+ * goldens rendered through the reference's ray_color / hittable_list / sphere / mt19937 with
+ * these materials plugged in (oracle/ref_harness.cpp; only the scatter bodies are ours). */
 enum { YK_MATERIAL_LAMBERTIAN = 0, YK_MATERIAL_METAL = 1, YK_MATERIAL_DIELECTRIC = 2 };
 
 /* Arithmetic of the per-sample path (the T of yk::render<T>, source.cpp:98-99).
@@ -79,10 +82,11 @@ enum {
   YK_FLAG_COUNT_WORK = 1u, /* count segments / sphere tests (ykgpu_get_stats)              */
   YK_FLAG_LINEAR_SCAN = 2u, /* closest hit by the reference's linear scan instead of the BVH
                               (same results; A/B and debugging)                              */
-  YK_FLAG_ONE_LANE = 4u     /* with COUNT_WORK, FP64 only (diagnostic): one lane per wave runs
+  YK_FLAG_ONE_LANE = 4u,    /* with COUNT_WORK, FP64 only (diagnostic): one lane per wave runs
                               paths, the other 63 idle.  The profiler's per-wave-instruction
                               counters (SQ_INSTS_VALU_FLOPS_FP64 ...) then read exactly the
                               instructions one lane executed: DESIGN.md §5 reconciliation   */
+  YK_FLAG_TRACE_RAYS = 8u   /* internal to ykgpu_render_trace                                 */
 };
 
 enum {
@@ -203,6 +207,16 @@ int ykgpu_render_async(ykgpu_context* ctx, const yk_render_params* params, void*
 /* Diagnostics: the per-pixel colour sum before to_color3b (source.cpp:137-167), 3 doubles per
  * pixel, row_count * W * 3 doubles, host buffer. */
 int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* params, double* sums_host);
+
+/* Verbose level 3 (raytracer.hpp:21-25: ray_color prints every ray it is called with, the one
+ * reaching depth 0 included).  Renders the rows of params (COUNT_WORK instance) and records, for
+ * every sample (index (row_t*W + x)*spp + s over the tile), the first max_rays rays of its path
+ * as 6 doubles each (origin xyz, direction xyz; FP32 rays are floats widened exactly) into
+ * rays_host[(index*max_rays + k)*6 ...] and the number of ray_color calls into counts_host[index]
+ * (which may exceed max_rays).  row_count * W * spp * max_rays * 48 bytes of device memory are
+ * used for the call, so callers render large images in row bands. */
+int ykgpu_render_trace(ykgpu_context* ctx, const yk_render_params* params, uint32_t max_rays,
+                       double* rays_host, uint32_t* counts_host);
 
 /* Diagnostics: the device's math::sqrt (math.hpp:10-19) -- the routine every length, root and
  * to_color3b in the render uses -- on n host doubles (in and out may alias).  The tests check it

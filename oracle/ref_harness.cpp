@@ -27,9 +27,13 @@
 //   render32 / samples32: the same with T = float (render<float>(); radius literals as T(...))
 //   render_x128 / samples_x128 / render32_x128 / samples32_x128: the engine is the reference's
 //     yk::xor128 (random.hpp:18-41) seeded with the same per-sample counter, in place of mt19937
+//   verbose <scene> W H spp depth seed0 level: the loop's console output at that verbose level,
+//     the rays printed by the reference's ray_color itself (the -l 3 fixture)
 //   render_file / samples_file (and the 32 / _x128 forms): <scene> is a scene file of 5, 24 or 48
 //     spheres (configs 2-5 content: dielectric, fuzzed metal, thin-lens camera; see below)
 #include <cmath>
+#include <iomanip>
+#include <iostream>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -442,9 +446,33 @@ int kat() {
   return 0;
 }
 
+// The console output of source.cpp's loop at verbose level `lv` (source.cpp:128-152 restated,
+// in its pixel / sample order) with the reference's own ray_color printing every ray it is called
+// with at level 3 (raytracer.hpp:21-25): the fixture of the drop-in's `-l 3`.
+template <class T, class E, class World, class Cam>
+int verbose_lines(const World& world, const Cam& cam, const job& j, std::uint32_t lv) {
+  std::ios::sync_with_stdio(false);
+  yk::verbose = lv;
+  const auto w = [](std::uint32_t n) { return (int)(std::ceil(std::log10(n)) - 1); };
+  for (std::uint32_t y = 0; y < j.H; ++y)
+    for (std::uint32_t x = 0; x < j.W; ++x) {
+      std::cout << "(row,col) : " << '(' << std::setw(w(j.H)) << y << ',' << std::setw(w(j.W)) << x << ')'
+                << std::endl;
+      for (std::uint32_t s = 0; s < j.spp; ++s) {
+        if (lv > 1)
+          std::cout << "(row,col,sam) : " << '(' << std::setw(w(j.H)) << y << ',' << std::setw(w(j.W)) << x << ','
+                    << std::setw(w(j.spp)) << s << ')' << std::endl;
+        sample_color<T, E>(world, cam, j, y, x, s, nullptr);
+      }
+    }
+  std::cout.flush();
+  return 0;
+}
+
 template <class T, class E, class World, class Cam = yk::camera<T>>
 int dispatch_world(const World& w, const char* mode, const job& j, int argc, char** argv, const Cam& cam = {}) {
   if (!std::strncmp(mode, "render", 6)) return render<T, E>(w, cam, j, argv[0], argc > 1 ? argv[1] : nullptr);
+  if (!std::strncmp(mode, "verbose", 7)) return verbose_lines<T, E>(w, cam, j, argc > 0 ? std::atoi(argv[0]) : 3);
   return samples<T, E>(w, cam, j, argc, argv);
 }
 

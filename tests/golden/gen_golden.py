@@ -101,6 +101,14 @@ CASES_FILE = [
     ("glass48.yks", 64, 36, 8, 200, 404, True, True, False),
 ]
 
+# verbose level 3 (-l 3): the loop's console lines with every ray printed by the reference's own
+# ray_color (raytracer.hpp:21-25); (scene or scene file, W, H, spp, depth, seed0, level, fp32)
+VERBOSE = [
+    ("ref4", 16, 9, 2, 50, 404, 3, False),
+    ("ref4", 16, 9, 2, 50, 404, 3, True),
+    ("final48.yks", 16, 9, 2, 50, 404, 3, False),
+]
+
 
 def write_scene_file(path, spheres, cam):
     """include/ykgpu.h yk_scene_write's format (%.17g round-trips every double)."""
@@ -239,6 +247,19 @@ def main():
             open(os.path.join(HERE, name + ".sums"), "wb").write(sums)
         manifest["cases"].append(entry)
         print("case", name, entry["rgb_sha256"][:16])
+    manifest["verbose"] = []
+    for scene, W, H, spp, depth, seed0, lv, f32 in VERBOSE:
+        is_file = scene.endswith(".yks")
+        mode = "verbose" + ("32" if f32 else "") + ("_file" if is_file else "")
+        out = subprocess.run([HARNESS, mode, os.path.join(HERE, scene) if is_file else scene, str(W), str(H),
+                              str(spp), str(depth), str(seed0), str(lv)], check=True, capture_output=True).stdout
+        name = case_name(scene[:-4] if is_file else scene, W, H, spp, depth, seed0, f32) + f"_l{lv}.txt"
+        open(os.path.join(HERE, name), "wb").write(out)
+        manifest["verbose"].append({"name": name, "scene": scene[:-4] if is_file else scene,
+                                    **({"scene_file": scene} if is_file else {}), "W": W, "H": H, "spp": spp,
+                                    "depth": depth, "seed0": seed0, "level": lv,
+                                    "precision": "fp32" if f32 else "fp64", "file": name})
+        print("verbose", name, out.count(b"\n"), "lines")
     cx = manifest["constexpr_build"]["rgb_sha256"]
     assert manifest["cases"][0]["rgb_sha256"] == cx, "harness disagrees with the constexpr build"
 

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = yk.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.ykgpu_abi_version() == 6
+    assert lib.ykgpu_abi_version() == 7
 
 
 def test_reference_camera_matches_camera_hpp():

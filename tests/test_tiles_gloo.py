@@ -1,7 +1,9 @@
 """N>1 path on CPU: world_size-2 (and 3) gloo processes each render their row tile — bands of
 rows dealt cyclically, and single rows — (the oracle stands in for the GPU here), gather to rank 0
 through uecraytracing_amd.tiles — the same code bench.py runs over RCCL — and rank 0's image must
-equal the single-process image."""
+equal the single-process image.  The tiles are CPU tensors, so TileGather.gather takes its RCCL
+branch's exact call — dist.gather(tile, list(gathered.unbind(0)), dst=0) then index_select — on
+gloo; only the device of the buffers differs from bench.py's N-GPU run."""
 import os
 import socket
 import sys

@@ -26,7 +26,7 @@ CLI_PATH = os.path.join(LIB_DIR, "raytrace")
 EXPORTS = (
     "ykgpu_abi_version", "ykgpu_last_error", "ykgpu_device_count", "ykgpu_context_create",
     "ykgpu_context_destroy", "ykgpu_set_scene", "ykgpu_render", "ykgpu_render_async",
-    "ykgpu_render_sums", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_sqrt_f32", "ykgpu_math_div", "yk_camera_reference", "yk_camera_look",
+    "ykgpu_render_sums", "ykgpu_render_trace", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_sqrt_f32", "ykgpu_math_div", "yk_camera_reference", "yk_camera_look",
     "yk_scene_build", "yk_scene_write", "yk_scene_read", "yk_image_height_for",
 )
 SCENE_DIR = os.path.join(PKG_DIR, "scenes")  # committed scene files of the BASELINE configs
@@ -66,6 +66,7 @@ def load_library():
         "ykgpu_render": ([c.c_void_p, P(RenderParams), c.c_void_p], c.c_int),
         "ykgpu_render_async": ([c.c_void_p, P(RenderParams), c.c_void_p, c.c_void_p], c.c_int),
         "ykgpu_render_sums": ([c.c_void_p, P(RenderParams), c.c_void_p], c.c_int),
+        "ykgpu_render_trace": ([c.c_void_p, P(RenderParams), c.c_uint32, c.c_void_p, c.c_void_p], c.c_int),
         "ykgpu_get_stats": ([c.c_void_p, P(RenderStats)], c.c_int),
         "ykgpu_math_sqrt": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
         "ykgpu_math_sqrt_f32": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
@@ -82,7 +83,7 @@ def load_library():
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
         f.argtypes, f.restype = args, res
-    if lib.ykgpu_abi_version() != 6:
+    if lib.ykgpu_abi_version() != 7:
         raise YkError("ABI version mismatch")
     _lib = lib
     return lib
@@ -172,6 +173,16 @@ class Renderer:
         out = np.empty((params.row_count, params.image_width, 3), np.float64)
         _check(self._lib.ykgpu_render_sums(self._ctx, ctypes.byref(params), out.ctypes.data))
         return out
+
+    def render_trace(self, params: RenderParams, max_rays: int):
+        """ray_color's rays (verbose level 3, raytracer.hpp:21-25) of every sample of the tile:
+        (rays float64[row_count, W, spp, max_rays, 6], counts uint32[row_count, W, spp])."""
+        shape = (params.row_count, params.image_width, params.samples_per_pixel)
+        rays = np.zeros(shape + (max_rays, 6), np.float64)
+        counts = np.zeros(shape, np.uint32)
+        _check(self._lib.ykgpu_render_trace(self._ctx, ctypes.byref(params), max_rays, rays.ctypes.data,
+                                            counts.ctypes.data))
+        return rays, counts
 
     def render_async(self, params: RenderParams, rgb_device_ptr: int, stream_ptr: int = 0):
         """Enqueue into device memory (e.g. a torch.uint8 CUDA tensor's data_ptr())."""

@@ -1,14 +1,20 @@
-// raytrace_main.cpp — the drop-in `raytrace` program: the reference's main()
+// raytrace_main.cpp — the repository's `raytrace` program: the reference's main()
 // (/root/reference/source.cpp:190-231) with render() (source.cpp:98-178) served by the GPU
-// through include/ykgpu.h.
+// through include/ykgpu.h, plus the runtime render parameters BASELINE configs 2-5 need.
 //
-// Kept from the reference: the options -h/--help, -v/--verbose, -o/--output, -l/--verbose-level
-// and the positional output file (source.cpp:197-216, cxxopts semantics: help or no output →
-// usage + exit 0; the last -l wins; an unknown option or a second positional argument is an
-// uncaught error → abort), the messages "rendering...", "rendering finished",
-// "write to file : <f>", "success" / "error" with exit 1 (source.cpp:114,174-175,223-230), the
-// default image (YK_IMAGE_WIDTH 400, YK_SPP 100, YK_MAX_DEPTH 50; source.cpp:43-53) and the
-// reference scene (source.cpp:103-112), built with the same yk calls.
+// This is NOT the reference's binary: its option parser and PNG writer are this file's own (the
+// reference's are cxxopts and stb_image_write, which this repository does not vendor).  The
+// reference's exact program — its cxxopts CLI, its stb PNG bytes — is the reference's own
+// source.cpp with oracle/source_cpp_ykgpu.patch applied (tests/test_cli.py
+// checks that build's PNG byte for byte against the reference's constexpr build).
+//
+// Kept from the reference: -h/--help, -v/--verbose, -o/--output, -l/--verbose-level and the
+// positional output (source.cpp:197-216: help or no output → usage + exit 0; the last -l wins),
+// the messages "rendering...", "rendering finished", "write to file : <f>", "success" / "error"
+// with exit 1 (source.cpp:114,174-175,223-230), the default image (YK_IMAGE_WIDTH 400, YK_SPP 100,
+// YK_MAX_DEPTH 50; source.cpp:43-53) and the reference scene (source.cpp:103-112), built with the
+// same yk calls.  A bad argument is reported with a message and exit status 2 (the reference
+// lets cxxopts' exception escape main and aborts).
 //
 // Added (render parameters are compile-time macros in the reference): --width, --spp,
 // --depth, --scene, --scene-seed, --scene-file, --save-scene, --seed0, --precision, --rng,
@@ -18,8 +24,9 @@
 // (source.cpp:159).  --precision fp32 renders render<float> (T = float, source.cpp:98);
 // --rng xor128 seeds the reference's yk::xor128 (random.hpp:18-41) per sample instead of
 // yk::mt19937.
-// Verbose output: levels 1-2 print the reference's per-pixel / per-sample lines after the GPU
-// render, in the same order; level 3 (per-ray dumps, raytracer.hpp:21-25) is not available.
+// Verbose output: the reference's per-pixel / per-sample lines (levels 1-2) and, at level 3, every
+// ray ray_color is called with (raytracer.hpp:21-25, from ykgpu_render_trace), in the
+// reference's order, after the GPU render.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -149,20 +156,17 @@ args parse(int argc, char** argv) {
         else throw option_error{std::string("Option '") + c + "' does not exist"};
       }
     } else {
-      // parse_positional({"output", "positional"}): the 2nd positional names an option that
-      // was never declared → cxxopts throws
+      // one positional argument, the output file (source.cpp:206)
       if (positional++ == 0) {
         a.output = s;
         a.have_output = true;
       } else {
-        throw option_error{"Option 'positional' does not exist"};
+        throw option_error{"unexpected second positional argument '" + s + "'"};
       }
     }
   }
   return a;
 }
-
-int digits(uint32_t n) { return (int)std::ceil(std::log10((double)n)) - 1; }  // source.cpp:130-133
 
 }  // namespace
 
@@ -174,10 +178,8 @@ int main(int argc, char* argv[]) {
   try {
     a = parse(argc, argv);
   } catch (const option_error& e) {
-    // the reference lets cxxopts' exception escape main: terminate → abort (exit 134)
-    std::cerr << "terminate called after throwing an instance of 'cxxopts::OptionException'\n"
-              << "  what():  " << e.what << std::endl;
-    std::abort();
+    std::cerr << "raytrace: " << e.what << " (see --help)" << std::endl;
+    return 2;
   }
   if (a.help || !a.have_output) {
     std::cout << kHelp << std::endl;
@@ -248,21 +250,14 @@ int main(int argc, char* argv[]) {
     }
     std::cout << "rendering..." << std::endl;
     image = gpu.render(W, H, a.spp, a.depth, seed0, ro);
+    const yk_render_stats st = gpu.stats();
     if (verbose) {
-      for (uint32_t y = 0; y < H; ++y)
-        for (uint32_t x = 0; x < W; ++x) {
-          std::cout << "(row,col) : " << '(' << std::setw(digits(H)) << y << ',' << std::setw(digits(W)) << x
-                    << ')' << '\n';
-          if (verbose > 1)
-            for (uint32_t s = 0; s < a.spp; ++s)
-              std::cout << "(row,col,sam) : " << '(' << std::setw(digits(H)) << y << ','
-                        << std::setw(digits(W)) << x << ',' << std::setw(digits(a.spp)) << s << ')' << '\n';
-        }
-      if (verbose > 2) std::cerr << "note: per-ray dumps (-l 3) are not produced by the GPU path\n";
+      ykgpu::render_options vo = ro;
+      vo.seed_key = st.seed_key;  // level 3 traces the same samples the image summed
+      gpu.print_verbose(std::cout, W, H, a.spp, a.depth, seed0, verbose, vo);
     }
     std::cout << "rendering finished" << std::endl;
     if (a.stats) {
-      const yk_render_stats st = gpu.stats();
       std::cerr << "kernels " << st.kernel_ms << " ms, " << (double)st.samples / st.kernel_ms / 1e3
                 << " Msamples/s, ";
       if (a.have_seed0)

@@ -119,6 +119,7 @@ constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
 #define YK_STR(x) YK_STR2(x)
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
+constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
 
 struct KernelArgs {
   yk_camera cam;
@@ -148,7 +149,22 @@ struct KernelArgs {
   uint32_t* mt_scratch;
   uint16_t* id_scratch;
   unsigned long long* counters;  // [segments, sphere_tests, sqrt_calls, mt_fallbacks, nodes]
+  double* trace;                 // YK_FLAG_TRACE_RAYS: rays [(q*spp + s)*trace_cap + k][6]
+  uint32_t* trace_counts;        //   ray_color calls per sample [q*spp + s]
+  uint32_t trace_cap, pad_t;
 };
+
+// -l 3 (raytracer.hpp:21-25): ray k of the path of the lane's sample slot (counting instance)
+template <class V>
+__device__ __forceinline__ void trace_ray(const KernelArgs& ka, uint32_t slot, uint32_t k, V o, V d) {
+  const uint32_t sl = slot / ka.npix_slots, q = ka.order[slot - sl * ka.npix_slots];
+  const size_t idx = (size_t)q * ka.spp + ka.s0 + sl;
+  if (k < ka.trace_cap) {
+    double* r = ka.trace + (idx * ka.trace_cap + k) * 6;
+    r[0] = o.x, r[1] = o.y, r[2] = o.z, r[3] = d.x, r[4] = d.y, r[5] = d.z;
+  }
+  ka.trace_counts[idx] = k + 1;
+}
 
 // Image row of tile row t (include/ykgpu.h yk_render_params: bands of 2^band_log2 rows, every
 // row_stride-th band; band_log2 = 0 is the plain strided row set)
@@ -508,6 +524,8 @@ void yk_render_persistent(KernelArgs ka) {
       in_path = true;
     }
     YK_STAMP(1);
+    // ray_color prints its ray before the depth test (raytracer.hpp:21-25)
+    if (kCount && (ka.flags & kFlagTrace) && in_path) trace_ray(ka, slot, ka.max_depth - depth, o, d);
 
     // ---- one segment of ray_color (raytracer.hpp:19-37) ----------------------------------
     // (a) closest hit: hittable_list::hit_impl (hittable_list.hpp:32-58) over
@@ -1033,6 +1051,8 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
       in_path = true;
     }
 
+    if (kCount && (ka.flags & kFlagTrace) && in_path) trace_ray(ka, slot, ka.max_depth - depth, o, d);
+
     // ---- closest hit (hittable_list.hpp:32-58 over sphere.hpp:25-48, in float)
     const bool alive = in_path && depth != 0;
     float T = INFINITY;
@@ -1337,6 +1357,9 @@ struct ykgpu_context {
   size_t sums_cap = 0;
   yk_render_stats stats{};
   bool stats_pending = false;
+  double* d_trace = nullptr;  // ykgpu_render_trace's buffers (only during that call)
+  uint32_t* d_trace_counts = nullptr;
+  uint32_t trace_cap = 0;
   std::chrono::steady_clock::time_point t0;
 };
 
@@ -1557,6 +1580,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.pixel_counter = ctx->d_counter;
 
   ka.counters = ctx->d_stats;
+  ka.trace = ctx->d_trace;
+  ka.trace_counts = ctx->d_trace_counts;
+  ka.trace_cap = ctx->trace_cap;
+  ka.pad_t = 0;
+  if ((ka.flags & YK_FLAG_TRACE_RAYS) && !(ctx->d_trace && (ka.flags & YK_FLAG_COUNT_WORK)))
+    return fail(YK_ERR_INVALID, "YK_FLAG_TRACE_RAYS is set by ykgpu_render_trace only");
   WarmArgs wa;
   wa.W = p->image_width;
   wa.spp = p->samples_per_pixel;
@@ -1978,6 +2007,36 @@ static int render_host(ykgpu_context* ctx, const yk_render_params* p, uint8_t* r
 int ykgpu_render(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_host) {
   if (!rgb_host) return fail(YK_ERR_INVALID, "null output");
   return render_host(ctx, p, rgb_host, nullptr);
+}
+
+int ykgpu_render_trace(ykgpu_context* ctx, const yk_render_params* p, uint32_t max_rays, double* rays_host,
+                       uint32_t* counts_host) {
+  int rc = check_params(ctx, p);
+  if (rc) return rc;
+  if (!max_rays || !rays_host || !counts_host) return fail(YK_ERR_INVALID, "null output or max_rays == 0");
+  const size_t n = (size_t)p->row_count * p->image_width * p->samples_per_pixel;
+  YK_HIP(hipSetDevice(ctx->device));
+  YK_HIP(hipMalloc(&ctx->d_trace, n * max_rays * 6 * sizeof(double)));
+  if (hipMalloc(&ctx->d_trace_counts, n * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipFree(ctx->d_trace);
+    ctx->d_trace = nullptr;
+    return fail(YK_ERR_NOMEM, "ykgpu_render_trace: ray counts");
+  }
+  ctx->trace_cap = max_rays;
+  yk_render_params q = *p;
+  q.flags |= YK_FLAG_COUNT_WORK | YK_FLAG_TRACE_RAYS;
+  rc = render_host(ctx, &q, nullptr, nullptr);
+  hipError_t e = hipSuccess;
+  if (!rc) e = hipMemcpy(rays_host, ctx->d_trace, n * max_rays * 6 * sizeof(double), hipMemcpyDeviceToHost);
+  if (!rc && e == hipSuccess) e = hipMemcpy(counts_host, ctx->d_trace_counts, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  (void)hipFree(ctx->d_trace);
+  (void)hipFree(ctx->d_trace_counts);
+  ctx->d_trace = nullptr;
+  ctx->d_trace_counts = nullptr;
+  ctx->trace_cap = 0;
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_render_trace: ") + hipGetErrorString(e));
+  return YK_OK;
 }
 
 int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* p, double* sums_host) {
