@@ -38,7 +38,10 @@ __device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.
 // below, under which the reference start is kept.  YK_NEWTON_REF_START=1 restores the
 // reference start everywhere (A/B timing).  The iteration bound only matters for NaN/inf.
 // YK_ABLATE (timing-only builds, tools/ablate.py; results are WRONG by design):
-//   1 = skip the MT warm-up walk, 2 = hardware sqrt instead of math::sqrt
+//   1 = skip the MT warm-up walk, 2 = hardware sqrt instead of math::sqrt, (8: phase stamps,
+//   no change of results), 16 = no thin-lens sampling, 32 = no attenuation unwind, 64 = no
+//   colour stores, 128 = no order / x_397 loads at a sample's start, 256 = lambertian scatter
+//   vector without MT draws
 #ifndef YK_ABLATE
 #define YK_ABLATE 0
 #endif
@@ -357,6 +360,13 @@ template <class G>
 __device__ __forceinline__ double uniform(G& g, double a, double b) {
   return (canonical(g) * (b - a)) + a;
 }
+// uniform_real_distribution::operator() on an already drawn canonical c: the same c*(b-a)+a
+__device__ __forceinline__ double uniform_of(double c, double a, double b) { return (c * (b - a)) + a; }
+// Whether the next two words may be drawn speculatively and then given back by restoring a copy
+// of the lane's engine: for mt19937 only inside the lazy cursors (the scratch engine's twist
+// rewrites its state in place); xor128's state is the copy.
+__device__ __forceinline__ bool rng_can_speculate(const MtLane& g) { return g.j + 2 <= kLazyDraws; }
+__device__ __forceinline__ bool rng_can_speculate(const X128Lane&) { return true; }
 // vec3::random(gen, -1, 1) (vec3.hpp:134-142): x, then y, then z
 template <class G>
 __device__ __forceinline__ v3 random_vec(G& g, double lo, double hi) {

@@ -111,6 +111,7 @@ constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (diagnostic
   } while (0)
 #endif
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
+
 #ifndef YK_CLAIM
 #define YK_CLAIM 512
 #endif
@@ -488,7 +489,11 @@ void yk_render_persistent(KernelArgs ka) {
     uint32_t qpix = 0;
     if (start) {
       const uint32_t sl = slot / ka.npix_slots;
+#if YK_ABLATE & 128
+      qpix = (slot - sl * ka.npix_slots) % (ka.W * ka.row_count);
+#else
       qpix = ka.order[slot - sl * ka.npix_slots];
+#endif
       start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
     if (start) {
@@ -496,8 +501,15 @@ void yk_render_persistent(KernelArgs ka) {
       const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       // seed (uint32 wrap, source.cpp:154-158); mt19937's x_397 comes from yk_mt_warmup
+#if YK_ABLATE & 128
+      if constexpr (std::is_same<Gen, ykd::MtLane>::value)
+        ykd::mt_start_from(g, ykd::sample_seed(0u, 0, ka.seed0, y, x, ka.W, ka.spp, s), slot * 2654435761u);
+      else
+        rng_start(g, ykd::sample_seed(0u, 0, ka.seed0, y, x, ka.W, ka.spp, s), ka, slot);
+#else
       rng_start(g, ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka,
                 slot);
+#endif
       // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
       const double u = ykd::div_markstein((double)x + ykd::uniform(g, 0, 1), (double)ka.W, ka.inv_w);
       const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1), (double)ka.H, ka.inv_h);
@@ -507,7 +519,7 @@ void yk_render_persistent(KernelArgs ka) {
       const double lens_r = ka.cam.lens_radius;
       d = ykd::sub(ykd::add(ykd::add(cam_llc, ykd::mul(cam_h, u)), ykd::mul(cam_v, v)), cam_o);
       o = cam_o;
-      if (lens_r > 0) {  // thin-lens extension: random_in_unit_disk by rejection
+      if (!(YK_ABLATE & 16) && lens_r > 0) {  // thin-lens extension: random_in_unit_disk by rejection
         double px, py;
         do {
           px = ykd::uniform(g, -1, 1);
@@ -768,11 +780,16 @@ void yk_render_persistent(KernelArgs ka) {
     }
     YK_STAMP(3);
 
-    // (b) shade.  Every live lane needs exactly one vector normalisation here — the sky's
-    //     normalized(dir) (raytracer.hpp:35), lambertian's random_unit_vector
-    //     (material.hpp:33-36), metal's / dielectric's normalized(dir) — so the Newton square
-    //     root of that length runs once, with all those lanes together, instead of once per
-    //     branch.  Each lane's own operation order is unchanged.
+    // (b) shade, material-uniform: every operation more than one material needs runs ONCE for all
+    //     the lanes that need it, instead of once per material branch (a wave holds every kind
+    //     almost every trip, so per-branch copies run one after the other):
+    //   * one block of canonicals: lambertian's vec3::random (3), the fuzzed metal's length factor
+    //     and vector (4), the dielectric's reflect-or-refract uniform (1, drawn speculatively:
+    //     given back when total internal reflection means the reference never draws it);
+    //   * one vector normalisation — the sky's normalized(dir) (raytracer.hpp:35), lambertian's
+    //     random_unit_vector (material.hpp:33-36), metal's / dielectric's normalized(dir);
+    //   * one more Newton square root: the fuzzed metal's |vector| or the dielectric's sin(theta).
+    //   Each lane's own operations and their order are the reference's.
     bool ended = in_path && !alive;
     double L_r = 0, L_g = 0, L_b = 0;
     if (alive) {
@@ -782,7 +799,6 @@ void yk_render_persistent(KernelArgs ka) {
       SphereMat m{};
       v3 p{0, 0, 0}, nrm{0, 0, 0};
       bool front = false;
-      v3 vn = d;
       if (hid >= 0) {
         sg = ka.geo[hid];
         m = ka.mat[hid];
@@ -791,12 +807,36 @@ void yk_render_persistent(KernelArgs ka) {
         const v3 outward = ykd::divs_fast(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
         front = ykd::dot(d, outward) < 0;
         nrm = front ? outward : ykd::neg(outward);
-        if (m.kind == YK_MATERIAL_LAMBERTIAN) vn = ykd::random_vec(g, -1, 1);  // vec3.hpp:134-142
       }
+      const bool lamb = hid >= 0 && m.kind == YK_MATERIAL_LAMBERTIAN;
+      const bool fuzzy = hid >= 0 && m.kind == YK_MATERIAL_METAL && m.fuzz > 0;
+      const bool diel = hid >= 0 && m.kind == YK_MATERIAL_DIELECTRIC;
+      const bool spec = diel && ykd::rng_can_speculate(g);
+      const Gen saved = g;  // the dielectric's engine before its speculative draw
+      const uint32_t ncan = lamb ? 3u : (fuzzy ? 4u : (spec ? 1u : 0u));
+      double c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+      if (ncan > 0) c0 = ykd::canonical(g);
+      if (ncan > 1) c1 = ykd::canonical(g);
+      if (ncan > 2) c2 = ykd::canonical(g);
+      if (ncan > 3) c3 = ykd::canonical(g);
+      // lambertian: vec3::random(gen, -1, 1), x then y then z (vec3.hpp:134-142); fuzzed metal:
+      // random(-1,1).normalize() * uniform(0.01,0.99) with the factor drawn first — g++, the
+      // reference's compiler, evaluates that product's operands right to left (pinned by the
+      // reference-harness goldens, tests/golden/gen_golden.py)
+      const v3 rv = lamb ? v3{ykd::uniform_of(c0, -1, 1), ykd::uniform_of(c1, -1, 1), ykd::uniform_of(c2, -1, 1)}
+                         : v3{ykd::uniform_of(c1, -1, 1), ykd::uniform_of(c2, -1, 1), ykd::uniform_of(c3, -1, 1)};
+      const v3 vn = lamb ? rv : d;
       const double len = ykd::nsqrt_c(ykd::len2(vn), n_ncall, n_nit);  // vec3::length(), vec3.hpp:127
       // vn / len is what every branch below divides (sky: d.y / len; lambertian: the random
       // vector; metal, dielectric: d), so it is computed once here, not once per branch
       const v3 un = ykd::divs_fast(vn, len);
+      double ct = 0;  // dielectric: cos(theta) = min(dot(-unit, n), 1)
+      if (diel) {
+        ct = ykd::dot(ykd::neg(un), nrm);
+        if (!(ct < 1.0)) ct = 1.0;
+      }
+      double sq2 = 0;  // fuzzed metal: |random vector|; dielectric: sin(theta)
+      if (fuzzy || diel) sq2 = ykd::nsqrt_c(fuzzy ? ykd::len2(rv) : 1.0 - ct * ct, n_ncall, n_nit);
       if (hid < 0) {
         // sky (raytracer.hpp:35-36): t = (normalized(dir).y + 1)/2, lerp white → (.5,.7,1)
         const double t = (un.y + 1.0) / 2;
@@ -814,14 +854,10 @@ void yk_render_persistent(KernelArgs ka) {
         } else if (m.kind == YK_MATERIAL_METAL) {  // material.hpp:67-75 (+ fuzz extension)
           if (kCount) ++n_metal;
           nd = ykd::reflect(un, nrm);
-          if (m.fuzz > 0) {  // + fuzz * random_in_unit_sphere (material.hpp:27-30)
+          if (fuzzy) {  // + fuzz * random_in_unit_sphere (material.hpp:27-30)
             if (kCount) ++n_fuzz;
-            // random(-1,1).normalize() * uniform(0.01,0.99): g++, the reference's compiler,
-            // evaluates the product's operands right to left, so the length factor is drawn
-            // first (pinned by the reference-harness goldens, tests/golden/gen_golden.py)
-            const double k = ykd::uniform(g, 0.01, 0.99);
-            v3 ru = ykd::random_vec(g, -1, 1);
-            ru = ykd::divs_fast(ru, ykd::nsqrt_c(ykd::len2(ru), n_ncall, n_nit));
+            const double k = ykd::uniform_of(c0, 0.01, 0.99);
+            const v3 ru = ykd::divs_fast(rv, sq2);
             nd = ykd::add(nd, ykd::mul(ykd::mul(ru, k), m.fuzz));
           }
           scattered = ykd::dot(nd, nrm) > 0;
@@ -830,11 +866,15 @@ void yk_render_persistent(KernelArgs ka) {
           push = false;
           const double ratio = front ? (1.0 / m.ior) : m.ior;
           const v3 unit = un;
-          double ct = ykd::dot(ykd::neg(unit), nrm);
-          if (!(ct < 1.0)) ct = 1.0;
-          const double sn = ykd::nsqrt_c(1.0 - ct * ct, n_ncall, n_nit);
+          const double sn = sq2;
           const bool cannot = ratio * sn > 1.0;
-          if (cannot || ykd::reflectance(ct, ratio) > ykd::uniform(g, 0, 1)) {
+          double u = 0;
+          if (cannot) {
+            if (spec) g = saved;  // `cannot || ...` never draws: give the word pair back
+          } else {
+            u = spec ? ykd::uniform_of(c0, 0, 1) : ykd::uniform(g, 0, 1);
+          }
+          if (cannot || ykd::reflectance(ct, ratio) > u) {
             nd = ykd::reflect(unit, nrm);
           } else {
             const v3 perp = ykd::mul(ykd::add(unit, ykd::mul(nrm, ct)), ratio);
@@ -863,23 +903,28 @@ void yk_render_persistent(KernelArgs ka) {
 
     if (ended) {
       // unwind: attenuation_k * (...) from the deepest scatter outwards (raytracer.hpp:31)
-      while (nstk > 0) {
+      auto pop = [&]() {
         const uint32_t id = st0 & 0xffffu;
         st0 = (st0 >> 16) | (st1 << 16);
         st1 = (st1 >> 16) | (st2 << 16);
         st2 = (st2 >> 16) | (st3 << 16);
         st3 = (st3 >> 16) | (nstk > kStackRegs ? ((uint32_t)id_spill[nstk - kStackRegs - 1] << 16) : 0u);
         --nstk;
-        const SphereMat m = ka.mat[id];
+        return id;
+      };
+      while (!(YK_ABLATE & 32) && nstk > 0) {
+        const SphereMat m = ka.mat[pop()];
         L_r = m.ar * L_r;
         L_g = m.ag * L_g;
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
       // the sample's colour; yk_reduce_samples adds them in sample order
-      ka.col[slot] = L_r;
-      ka.col[(size_t)ka.nsl + slot] = L_g;
-      ka.col[2 * (size_t)ka.nsl + slot] = L_b;
+      if (!(YK_ABLATE & 64)) {
+        ka.col[slot] = L_r;
+        ka.col[(size_t)ka.nsl + slot] = L_g;
+        ka.col[2 * (size_t)ka.nsl + slot] = L_b;
+      }
       in_path = false;
     }
     YK_STAMP(5);
