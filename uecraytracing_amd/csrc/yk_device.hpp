@@ -284,6 +284,18 @@ __device__ __noinline__ uint32_t mt_slow(uint32_t* st, uint32_t seed, uint32_t j
   return st[idx];
 }
 
+// The lazy cursors' draw without the check for the scratch engine: only for callers that know
+// every lane drawing here has j + words <= kLazyDraws (rng_lazy_ok)
+__device__ __forceinline__ uint32_t mt_next_lazy(MtLane& g) {
+  const uint32_t z = g.b ^ mt_mix(g.a0, g.a1);
+  g.a0 = g.a1;
+  g.a1 = mt_seed_step(g.a1, g.j + 2);
+  g.b = mt_seed_step(g.b, g.j + kMtM + 1);
+  ++g.j;
+  return mt_temper(z);
+}
+__device__ __forceinline__ bool rng_lazy_ok(const MtLane& g, uint32_t words) { return g.j + words <= kLazyDraws; }
+
 __device__ __forceinline__ uint32_t mt_next(MtLane& g) {
   uint32_t z;
   if (g.j < kLazyDraws) {
@@ -338,17 +350,21 @@ __device__ __forceinline__ uint32_t x128_next(X128Lane& g) {  // operator(), :34
 }
 __device__ __forceinline__ bool mt_used_fallback(const X128Lane&) { return false; }
 
-// One 32-bit draw of the lane's engine
-__device__ __forceinline__ uint32_t rng_next(MtLane& g) { return mt_next(g); }
+__device__ __forceinline__ bool rng_lazy_ok(const X128Lane&, uint32_t) { return true; }
+
+// One 32-bit draw of the lane's engine (kLazy: the caller has checked rng_lazy_ok)
+template <bool kLazy = false>
+__device__ __forceinline__ uint32_t rng_next(MtLane& g) { return kLazy ? mt_next_lazy(g) : mt_next(g); }
+template <bool kLazy = false>
 __device__ __forceinline__ uint32_t rng_next(X128Lane& g) { return x128_next(g); }
 
 // generate_canonical<double,53> (random.hpp:161-183): two draws (both engines have
 // min 0, max 2^32-1, so r = 2^32 and m = 2), sum = u0 + u1*2^32 rounded once, divided by 2^64
 // (exact), clamped to 1 - eps/2.
-template <class G>
+template <bool kLazy = false, class G>
 __device__ __forceinline__ double canonical(G& g) {
-  const double u0 = (double)rng_next(g);
-  const double u1 = (double)rng_next(g);
+  const double u0 = (double)rng_next<kLazy>(g);
+  const double u1 = (double)rng_next<kLazy>(g);
   double sum = u0;
   sum = sum + u1 * 4294967296.0;
   double r = sum / 18446744073709551616.0;
@@ -356,9 +372,9 @@ __device__ __forceinline__ double canonical(G& g) {
   return r;
 }
 // uniform_real_distribution::operator() (random.hpp:273-278): c*(b-a)+a
-template <class G>
+template <bool kLazy = false, class G>
 __device__ __forceinline__ double uniform(G& g, double a, double b) {
-  return (canonical(g) * (b - a)) + a;
+  return (canonical<kLazy>(g) * (b - a)) + a;
 }
 // uniform_real_distribution::operator() on an already drawn canonical c: the same c*(b-a)+a
 __device__ __forceinline__ double uniform_of(double c, double a, double b) { return (c * (b - a)) + a; }

@@ -511,8 +511,9 @@ void yk_render_persistent(KernelArgs ka) {
                 slot);
 #endif
       // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
-      const double u = ykd::div_markstein((double)x + ykd::uniform(g, 0, 1), (double)ka.W, ka.inv_w);
-      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform(g, 0, 1), (double)ka.H, ka.inv_h);
+      // (a fresh engine: its first words never need the scratch engine)
+      const double u = ykd::div_markstein((double)x + ykd::uniform<true>(g, 0, 1), (double)ka.W, ka.inv_w);
+      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform<true>(g, 0, 1), (double)ka.H, ka.inv_h);
       // camera::get_ray (camera.hpp:29-32): llc + u*horizontal + v*vertical (- origin)
       const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
       const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
@@ -815,10 +816,18 @@ void yk_render_persistent(KernelArgs ka) {
       const Gen saved = g;  // the dielectric's engine before its speculative draw
       const uint32_t ncan = lamb ? 3u : (fuzzy ? 4u : (spec ? 1u : 0u));
       double c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-      if (ncan > 0) c0 = ykd::canonical(g);
-      if (ncan > 1) c1 = ykd::canonical(g);
-      if (ncan > 2) c2 = ykd::canonical(g);
-      if (ncan > 3) c3 = ykd::canonical(g);
+      if (__ballot(ncan > 0 && !ykd::rng_lazy_ok(g, 2 * ncan)) == 0) {
+        // (almost always) no lane of the wave reaches the scratch engine's words: no checks
+        if (ncan > 0) c0 = ykd::canonical<true>(g);
+        if (ncan > 1) c1 = ykd::canonical<true>(g);
+        if (ncan > 2) c2 = ykd::canonical<true>(g);
+        if (ncan > 3) c3 = ykd::canonical<true>(g);
+      } else {
+        if (ncan > 0) c0 = ykd::canonical(g);
+        if (ncan > 1) c1 = ykd::canonical(g);
+        if (ncan > 2) c2 = ykd::canonical(g);
+        if (ncan > 3) c3 = ykd::canonical(g);
+      }
       // lambertian: vec3::random(gen, -1, 1), x then y then z (vec3.hpp:134-142); fuzzed metal:
       // random(-1,1).normalize() * uniform(0.01,0.99) with the factor drawn first — g++, the
       // reference's compiler, evaluates that product's operands right to left (pinned by the
