@@ -71,8 +71,11 @@ struct alignas(16) SphereMat {
 };
 static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 
+// One 768-thread workgroup per CU (12 waves, 3 per SIMD): the scene is copied into LDS once per
+// CU instead of once per 256-thread block, which leaves room for the shading tables (sphere
+// geometry and materials in tuple order) beside the BVH and full-depth traversal stacks
 #ifndef YK_BLOCK
-#define YK_BLOCK 256
+#define YK_BLOCK 768
 #endif
 #ifndef YK_WAVES_PER_EU
 #define YK_WAVES_PER_EU 0
@@ -139,6 +142,7 @@ struct KernelArgs {
   int32_t bvh_root;
   uint32_t n_nodes;
   uint32_t lds_geo_off, lds_ids_off, lds_stack_off, stack_cap;  // stack_cap: entries a lane may hold
+  uint32_t lds_tgeo_off, lds_mat_off;  // FP64 kernel: tuple-order geometry / materials in LDS
   const DevNode* __restrict__ nodes;  // child links are byte offsets from nodes
   const SphereGeo* __restrict__ leaf_geo;  // spheres in BVH leaf order
   const uint32_t* __restrict__ leaf_ids;   // leaf slot → tuple index
@@ -428,13 +432,17 @@ void yk_render_persistent(KernelArgs ka) {
   const char* __restrict__ nodes = (const char*)ka.nodes;
   const SphereGeo* __restrict__ leaf_geo = ka.leaf_geo;
   const uint32_t* __restrict__ leaf_ids = ka.leaf_ids;
+  const SphereGeo* __restrict__ geo = ka.geo;  // tuple order: candidates' roots, hit records
+  const SphereMat* __restrict__ mat = ka.mat;  // shading, attenuation unwind
   if (kSceneInLds) {
-    const uint4* src[3] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids};
-    const uint32_t off[3] = {0u, ka.lds_geo_off, ka.lds_ids_off};
-    const uint32_t n16[3] = {(ka.n_nodes * (uint32_t)sizeof(DevNode) + 15u) / 16u, ka.nspheres * 2u,
-                             (ka.nspheres + 3u) / 4u};
+    // the BVH, its leaf geometry and ids, and (tuple order) the geometry and materials
+    const uint4* src[5] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids,
+                           (const uint4*)ka.geo, (const uint4*)ka.mat};
+    const uint32_t off[5] = {0u, ka.lds_geo_off, ka.lds_ids_off, ka.lds_tgeo_off, ka.lds_mat_off};
+    const uint32_t n16[5] = {(ka.n_nodes * (uint32_t)sizeof(DevNode) + 15u) / 16u, ka.nspheres * 2u,
+                             (ka.nspheres + 3u) / 4u, ka.nspheres * 2u, ka.nspheres * 4u};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 5; ++k) {
       uint4* dst = (uint4*)(smem + off[k]);
       for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlock) dst[i] = src[k][i];
     }
@@ -442,6 +450,8 @@ void yk_render_persistent(KernelArgs ka) {
     nodes = smem;
     leaf_geo = (const SphereGeo*)(smem + ka.lds_geo_off);
     leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
+    geo = (const SphereGeo*)(smem + ka.lds_tgeo_off);
+    mat = (const SphereMat*)(smem + ka.lds_mat_off);
   }
   int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlock]
   // YK_FLAG_ONE_LANE (counting instance only): lanes 1..63 leave here, after the block's last
@@ -764,10 +774,10 @@ void yk_render_persistent(KernelArgs ka) {
           // same for every candidate, so its refined reciprocal is computed once
           const bool a_ok = ykd::div_range(a);
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
-          if (nc > 0 && l0 <= ustar_f) exact_candidate(ka.geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
-          if (nc > 1 && l1 <= ustar_f) exact_candidate(ka.geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
-          if (nc > 2 && l2 <= ustar_f) exact_candidate(ka.geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
-          if (nc > 3 && l3 <= ustar_f) exact_candidate(ka.geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 1 && l1 <= ustar_f) exact_candidate(geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 2 && l2 <= ustar_f) exact_candidate(geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 3 && l3 <= ustar_f) exact_candidate(geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
         }
       }
       if (linear) {
@@ -801,8 +811,8 @@ void yk_render_persistent(KernelArgs ka) {
       v3 p{0, 0, 0}, nrm{0, 0, 0};
       bool front = false;
       if (hid >= 0) {
-        sg = ka.geo[hid];
-        m = ka.mat[hid];
+        sg = geo[hid];
+        m = mat[hid];
         // hit record (sphere.hpp:41-45, hittable.hpp:23-27)
         p = ykd::add(o, ykd::mul(d, T));
         const v3 outward = ykd::divs_fast(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
@@ -922,7 +932,7 @@ void yk_render_persistent(KernelArgs ka) {
         return id;
       };
       while (!(YK_ABLATE & 32) && nstk > 0) {
-        const SphereMat m = ka.mat[pop()];
+        const SphereMat m = mat[pop()];
         L_r = m.ar * L_r;
         L_g = m.ag * L_g;
         L_b = m.ab * L_b;
@@ -1362,6 +1372,7 @@ struct DevTree {
   double origin_bound = 0;  // |o|_inf beyond which a ray takes the linear scan (< 0: every ray)
   bool in_lds = false;
   uint32_t lds_bytes = 0, geo_off = 0, ids_off = 0, stack_off = 0, stack_cap = 0, stack_entries = 0;
+  uint32_t tgeo_off = 0, mat_off = 0;  // shading tables in LDS (FP64 kernel), 0: none
   int grid = 0;  // persistent blocks: occupancy x CUs
   void release() {
     (void)hipFree(nodes);
@@ -1621,6 +1632,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.n_nodes = tree.n_nodes;
   ka.lds_geo_off = tree.geo_off;
   ka.lds_ids_off = tree.ids_off;
+  ka.lds_tgeo_off = tree.tgeo_off;
+  ka.lds_mat_off = tree.mat_off;
   ka.lds_stack_off = tree.stack_off;
   ka.stack_cap = tree.stack_cap;
   ka.nodes = tree.nodes;
@@ -1803,8 +1816,8 @@ int finish_stats(ykgpu_context* ctx) {
 // kernel's leaves read (`elem` bytes per sphere), stored in leaf order; kern_lds / kern_glob are
 // the kernel instances that read the tree from LDS / global memory (for the occupancy).
 int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
-                double cam_ext, const ykbvh::Options& opt, const void* geo, size_t elem, RenderKernel kern_lds,
-                RenderKernel kern_glob) {
+                double cam_ext, const ykbvh::Options& opt, const void* geo, size_t elem, size_t table_bytes,
+                RenderKernel kern_lds, RenderKernel kern_glob) {
   const uint32_t count = (uint32_t)radii.size();
   const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
   if (bvh.depth > ykbvh::kMaxDepth) return fail(YK_ERR_INVALID, "BVH deeper than the traversal stack");
@@ -1832,21 +1845,27 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   t.depth = bvh.depth;
   t.origin_bound = bvh.origin_bound;
   t.n_nodes = (uint32_t)snodes.size();
-  // LDS layout: [nodes][leaf geometry][leaf ids][traversal stacks]
+  // LDS layout: [nodes][leaf geometry][leaf ids][tuple-order geometry][materials][traversal
+  // stacks].  The tables (table_bytes per sphere: the FP64 kernel's candidate and shading reads,
+  // 0 for the FP32 kernel) go wherever the tree goes: the LDS instance reads both from LDS
   auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t scene_bytes = a16(t.n_nodes * sizeof(DevNode)) + a16(count * elem) + a16(count * sizeof(uint32_t));
-  t.in_lds = scene_bytes <= 64 * 1024;
+  const size_t tgeo_bytes = table_bytes ? a16(count * sizeof(SphereGeo)) : 0;
+  const size_t mat_bytes = table_bytes ? a16(count * sizeof(SphereMat)) : 0;
+  // a CU holds 768 / kBlock workgroups (3 waves per SIMD); 2 KB below the share: the hardware's
+  // allocation granularity (3 blocks of 54144 bytes measured only 2 resident per CU)
+  const size_t budget = (size_t)160 * 1024 / std::max(1, 768 / kBlock) - 2048;
+  const size_t min_stacks = (size_t)12 * kBlock * 4;
+  t.in_lds = scene_bytes + tgeo_bytes + mat_bytes + min_stacks <= budget;
+  const size_t tables = t.in_lds ? tgeo_bytes + mat_bytes : 0;
 #if YK_WIDE
-  // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries), but
-  // the stacks share LDS with the scene, so the capacity is what still fits 3 blocks per CU (at
-  // least 8); a lane that would exceed it abandons the traversal for the exact linear scan.
-  // Pushes write unconditionally at the current top (up to 3 past the capacity): +4 entries.
+  // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries); the
+  // capacity is what still fits the budget (at least 8); a lane that would exceed it abandons the
+  // traversal for the exact linear scan.  Pushes write unconditionally at the current top (up to
+  // 3 past the capacity): +4 entries.
   {
-    // (2 KB below a third of the CU's LDS: the hardware's allocation granularity — 3 blocks of
-    // 54144 bytes measured only 2 resident per CU, with the grid still sized for 3)
-    const size_t budget = (size_t)160 * 1024 / 3 - 2048;
-    const size_t used = t.in_lds ? scene_bytes : 0;
-    const uint32_t fit = used + 12 * kBlock * 4 <= budget ? (uint32_t)((budget - used) / (kBlock * 4)) : 12u;
+    const size_t used = t.in_lds ? scene_bytes + tables : 0;
+    const uint32_t fit = used + min_stacks <= budget ? (uint32_t)((budget - used) / (kBlock * 4)) : 12u;
     t.stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
     t.stack_entries = t.stack_cap + 4;
   }
@@ -1856,7 +1875,9 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
 #endif
   t.geo_off = (uint32_t)a16(t.n_nodes * sizeof(DevNode));
   t.ids_off = t.geo_off + (uint32_t)a16(count * elem);
-  t.stack_off = t.in_lds ? (uint32_t)scene_bytes : 0u;
+  t.tgeo_off = t.in_lds && table_bytes ? (uint32_t)scene_bytes : 0u;
+  t.mat_off = t.in_lds && table_bytes ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
+  t.stack_off = t.in_lds ? (uint32_t)(scene_bytes + tables) : 0u;
   t.lds_bytes = t.stack_off + t.stack_entries * kBlock * (uint32_t)sizeof(int32_t);
   int per_cu = 0;
   const hipError_t e =
@@ -1997,12 +2018,12 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   ykbvh::Options bopt;
   if (const char* e = std::getenv("YKGPU_BVH_LEAF")) bopt.max_leaf = std::max(1, std::min(15, std::atoi(e)));
   int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, geo.data(), sizeof(SphereGeo),
-                       fp64_kernel(true, 0), fp64_kernel(false, 0));
+                       sizeof(SphereGeo) + sizeof(SphereMat), fp64_kernel(true, 0), fp64_kernel(false, 0));
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
   fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
   fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
-  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4),
+  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4), 0,
                    f32_kernel(true, 0), f32_kernel(false, 0));
   if (rc) return rc;
   // the float bound assumes neither underflow nor overflow: a scene outside that
