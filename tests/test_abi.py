@@ -83,3 +83,31 @@ def test_invalid_arguments_are_reported():
     assert lib.ykgpu_context_create(0, None) == 1
     assert b"null" in lib.ykgpu_last_error()
     assert lib.ykgpu_set_scene(None, None, 0, None) == 1
+
+
+def test_fastdiv_magic_numbers_divide_exactly():
+    """The kernels divide 31-bit slot and pixel indices by runtime-invariant divisors with the
+    host's magic numbers (ykgpu_render.hip fastdiv / fdiv): q = (n * m) >> sh, sh = 31 + ceil(log2 d),
+    m = ceil(2^sh / d).  Restated here and checked against integer division on every divisor kind
+    the renderer meets (image widths, padded pixel counts) and random ones, at the numerator's
+    extremes and at random numerators."""
+    import random
+
+    def magic(d):
+        l = 0
+        while (1 << l) < d:
+            l += 1
+        sh = 31 + l
+        m = ((1 << sh) + d - 1) // d
+        assert m < (1 << 32)
+        return m, sh
+
+    rng = random.Random(3)
+    divisors = [1, 2, 3, 7, 16, 200, 400, 800, 1920, 3840, 2073600, 2078720, 8294400, (1 << 31) - 1, 1 << 30]
+    divisors += [rng.randrange(1, 1 << 31) for _ in range(2000)] + [rng.randrange(1, 1 << 12) for _ in range(2000)]
+    for d in divisors:
+        m, sh = magic(d)
+        ns = [0, 1, d - 1, d, d + 1, (1 << 31) - 1, (1 << 31) - 2] + [rng.randrange(0, 1 << 31) for _ in range(200)]
+        for n in ns:
+            if 0 <= n < (1 << 31):
+                assert (n * m) >> sh == n // d, (n, d)

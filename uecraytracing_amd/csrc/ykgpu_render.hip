@@ -133,6 +133,7 @@ struct KernelArgs {
   // A launch renders samples [s0, s0 + nsl / npix_slots) of every pixel: sample slot
   // i = s_local * npix_slots + p is sample s0 + s_local of tile pixel order[p].
   uint32_t s0, nsl, npix_slots, seed_mode;  // seed_mode: YK_SEED_*
+  uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
   uint64_t seed_key;
   const uint32_t* __restrict__ order;  // p → tile pixel (kNoPixel: empty slot of an edge block)
   const uint32_t* __restrict__ warm;   // x_397 per sample slot of the launch
@@ -149,7 +150,7 @@ struct KernelArgs {
   const SphereGeo* __restrict__ geo;
   const SphereMat* __restrict__ mat;
   const float4* __restrict__ geo_f;  // FP32 path: (cx, cy, cz, r*r) rounded to float, tuple order
-  double* col;                       // sample colours, SoA: col[c * nsl + i]
+  double* col;                       // sample colours: kColStride doubles per slot (colour_store)
   uint32_t* pixel_counter;           // sample-slot counter
   uint32_t* mt_scratch;
   uint16_t* id_scratch;
@@ -169,6 +170,14 @@ __device__ __forceinline__ void trace_ray(const KernelArgs& ka, uint32_t slot, u
     r[0] = o.x, r[1] = o.y, r[2] = o.z, r[3] = d.x, r[4] = d.y, r[5] = d.z;
   }
   ka.trace_counts[idx] = k + 1;
+}
+
+// floor(n / d) for n < 2^31 with the host's magic numbers (fastdiv): ((uint64) n * m) >> sh, where
+// l = ceil(log2 d), sh = 31 + l, m = ceil(2^sh / d) < 2^32 — exact for every 31-bit n (the
+// round-up error n * (m d - 2^sh) / (d 2^sh) < 2^31 d / (d 2^sh) * d / 2^l <= 1/d).  A runtime
+// divisor otherwise costs the ~20-instruction float-reciprocal sequence per division.
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t sh) {
+  return (uint32_t)(((uint64_t)n * m) >> sh);
 }
 
 // Image row of tile row t (include/ykgpu.h yk_render_params: bands of 2^band_log2 rows, every
@@ -274,6 +283,7 @@ constexpr uint32_t kNoPixel = 0xffffffffu;
 // one 16-B store.  out[i] = x_397(seed(i)), i = (pix - pix_base) * spp + s.
 struct WarmArgs {
   uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode, band_log2;
+  uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
   uint64_t seed_key;
   const uint32_t* order;
   uint64_t n;  // sample slots in the launch
@@ -287,11 +297,11 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint64_t i = i0 + k < wa.n ? i0 + k : wa.n - 1;
-      const uint32_t sl = (uint32_t)(i / wa.npix_slots), pp = (uint32_t)(i - (uint64_t)sl * wa.npix_slots);
+      const uint32_t sl = fdiv((uint32_t)i, wa.nps_m, wa.nps_sh), pp = (uint32_t)i - sl * wa.npix_slots;
       const uint32_t q = wa.order[pp];
       const uint32_t pix = q == kNoPixel ? 0u : q;
       const uint32_t sm = wa.s0 + sl;
-      const uint32_t tr = pix / wa.W, xx = pix - tr * wa.W;
+      const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh), xx = pix - tr * wa.W;
       const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
       x[k] = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, sm);
     }
@@ -308,12 +318,31 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 // into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
 
+// A sample's colour record: r, g, b as one aligned 32-byte record per sample slot (one 16-byte
+// and one 8-byte store, the whole record in one 32-byte sector; YK_COL_AOS=0: 24-byte records,
+// three 8-byte stores).  yk_reduce_samples reads the records of consecutive slots, coalesced.
+#ifndef YK_COL_AOS
+#define YK_COL_AOS 1
+#endif
+constexpr size_t kColStride = YK_COL_AOS ? 4 : 3;
+__device__ __forceinline__ void colour_store(double* col, uint32_t slot, double r, double g, double b) {
+#if YK_COL_AOS
+  double* rec = col + (size_t)slot * kColStride;
+  *(double2*)rec = make_double2(r, g);
+  rec[2] = b;
+#else
+  col[(size_t)slot * kColStride + 0] = r;
+  col[(size_t)slot * kColStride + 1] = g;
+  col[(size_t)slot * kColStride + 2] = b;
+#endif
+}
+
 // Ordered sum of a launch's sample colours per pixel: pixel_color of source.cpp:137-167 is the
 // left fold ((0 + c_0) + c_1) + ... in sample order, continued across launches through acc; after
 // the last launch, to_color3b (source.cpp:73-83): /spp, math::sqrt, clamp [0, .999], *256,
 // truncate.  One thread per processing slot, coalesced over the SoA colours.
 struct ReduceArgs {
-  const double* col;  // col[c * nsl + s_local * npix_slots + p]
+  const double* col;  // col[(s_local * npix_slots + p) * kColStride + c]
   double* acc;        // running sums, acc[c * npix_slots + p]
   const uint32_t* order;
   uint8_t* rgb;
@@ -332,7 +361,7 @@ __global__ __launch_bounds__(256) void yk_reduce_samples(ReduceArgs ra) {
   for (uint32_t k = 0; k < ra.ks; ++k) {
     const size_t i = (size_t)k * ra.npix_slots + p;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[(size_t)c * ra.nsl + i];
+    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[i * kColStride + c];
   }
   if (!ra.last) {
 #pragma unroll
@@ -498,7 +527,7 @@ void yk_render_persistent(KernelArgs ka) {
     bool start = !in_path;
     uint32_t qpix = 0;
     if (start) {
-      const uint32_t sl = slot / ka.npix_slots;
+      const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
 #if YK_ABLATE & 128
       qpix = (slot - sl * ka.npix_slots) % (ka.W * ka.row_count);
 #else
@@ -507,8 +536,8 @@ void yk_render_persistent(KernelArgs ka) {
       start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
     if (start) {
-      const uint32_t s = ka.s0 + slot / ka.npix_slots;
-      const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
+      const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
+      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       // seed (uint32 wrap, source.cpp:154-158); mt19937's x_397 comes from yk_mt_warmup
 #if YK_ABLATE & 128
@@ -940,9 +969,7 @@ void yk_render_persistent(KernelArgs ka) {
       if (ykd::mt_used_fallback(g)) ++n_fb;
       // the sample's colour; yk_reduce_samples adds them in sample order
       if (!(YK_ABLATE & 64)) {
-        ka.col[slot] = L_r;
-        ka.col[(size_t)ka.nsl + slot] = L_g;
-        ka.col[2 * (size_t)ka.nsl + slot] = L_b;
+        colour_store(ka.col, slot, L_r, L_g, L_b);
       }
       in_path = false;
     }
@@ -1082,13 +1109,13 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
     bool start = !in_path;
     uint32_t qpix = 0;
     if (start) {
-      const uint32_t sl = slot / ka.npix_slots;
+      const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
       qpix = ka.order[slot - sl * ka.npix_slots];
       start = qpix != kNoPixel;
     }
     if (start) {
-      const uint32_t s = ka.s0 + slot / ka.npix_slots;
-      const uint32_t tr = qpix / ka.W, x = qpix - tr * ka.W;
+      const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
+      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       rng_start(g, ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka, slot);
       // (x + U01) / W with x, W unsigned → float (uniform_real_distribution<float>)
@@ -1322,9 +1349,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
-      ka.col[slot] = L_r;
-      ka.col[(size_t)ka.nsl + slot] = L_g;
-      ka.col[2 * (size_t)ka.nsl + slot] = L_b;
+      colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
   }
@@ -1390,7 +1415,7 @@ struct ykgpu_context {
   DevTree t64, t32;  // the FP64 and FP32 kernels' trees over the current scene
   size_t scratch_lanes = 0;
   uint32_t* d_warm = nullptr;  // x_397 per sample slot of one launch
-  double* d_col = nullptr;     // sample colours of one launch (SoA)
+  double* d_col = nullptr;     // sample colours of one launch (kColStride doubles per slot)
   double* d_acc = nullptr;     // running per-pixel sums between launches
   size_t col_cap = 0, acc_cap = 0;
   uint32_t* d_order = nullptr;  // processing slot → tile pixel, for (order_w, order_rows)
@@ -1433,6 +1458,14 @@ namespace {
 uint64_t host_row_y(const yk_render_params* p, uint32_t t) {
   const uint32_t L = p->row_band_log2;
   return (uint64_t)p->row_begin + ((((uint64_t)(t >> L)) * p->row_stride) << L) + (t & ((1u << L) - 1u));
+}
+
+// Magic numbers of fdiv (kernel side) for a divisor 1 <= d < 2^31
+void fastdiv(uint32_t d, uint32_t& m, uint32_t& sh) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  sh = 31 + l;
+  m = (uint32_t)(((1ull << sh) + d - 1) / d);
 }
 
 int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
@@ -1575,8 +1608,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // for the per-rank tiles of N GPUs.
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
   const uint32_t spp = p->samples_per_pixel;
+  // (slots of a launch stay below 2^31: the kernels' fdiv takes 31-bit numerators)
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>({spp, kColourBytes / (24ull * nps), kLaunchSpp}));
+      1, std::min<uint64_t>({spp, kColourBytes / (8ull * kColStride * nps), kLaunchSpp, ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
   for (uint32_t s0 = 0, k = std::min(kFirstLaunch, kmax); s0 < spp;) {
     uint32_t take = std::min(k, spp - s0);
@@ -1606,7 +1640,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (4ull * nps * K)));
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K, sizeof(uint32_t)))) return rc;
   // two colour buffers: reduce c (stream red) overlaps render c + 1
-  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)2 * nps * K * 3, sizeof(double)))) return rc;
+  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)2 * nps * K * kColStride, sizeof(double)))) return rc;
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
@@ -1662,10 +1696,16 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.band_log2 = p->row_band_log2;
   wa.out = ctx->d_warm;
   wa.npix_slots = nps;
+  fastdiv(nps, wa.nps_m, wa.nps_sh);
+  fastdiv(p->image_width, wa.w_m, wa.w_sh);
   wa.seed_mode = p->seed_mode;
   wa.seed_key = seed_key;
   wa.order = ctx->d_order;
   ka.npix_slots = nps;
+  ka.nps_m = wa.nps_m;
+  ka.nps_sh = wa.nps_sh;
+  ka.w_m = wa.w_m;
+  ka.w_sh = wa.w_sh;
   ka.pad_n = 0;
   ReduceArgs ra;
   ra.acc = ctx->d_acc;
@@ -1721,7 +1761,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     hipEvent_t* ev = &ctx->lev[6 * c];
     const uint32_t s0 = sched[c].first, ks = sched[c].second;
     const uint32_t nsl = nps * ks;
-    double* col = ctx->d_col + (size_t)(c % 2) * nps * K * 3;
+    double* col = ctx->d_col + (size_t)(c % 2) * nps * K * kColStride;
     ka.s0 = s0;
     ka.nsl = nsl;
     ka.col = col;
