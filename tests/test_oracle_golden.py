@@ -84,6 +84,27 @@ def test_newton_sqrt_result_is_path_independent():
             assert _newton_from(s, start) == ref, (s.hex(), start.hex())
 
 
+def test_newton_sqrt_one_step_from_ieee_sqrt():
+    """The device's math::sqrt for s in [2^-400, 2^400] (yk_device.hpp nsqrt_impl): ONE step
+    (r + s/r)/2 from the correctly rounded r = sqrt(s) equals the reference loop from s/2
+    (math.hpp:10-19).  Here on every binade boundary +- 48 ulp and 2e5 random values (the build
+    also ran 4.2e8 values in C: DESIGN.md §3)."""
+    import math
+    import random
+    rng = random.Random(11)
+    values = [math.ldexp(1.0 + rng.random(), rng.randrange(-400, 401)) for _ in range(150000)]
+    values += [rng.random() * 4.0 for _ in range(50000)]
+    for k in range(-400, 401):
+        up = dn = math.ldexp(1.0, k)
+        for _ in range(48):
+            values += [up, dn]
+            up, dn = math.nextafter(up, math.inf), math.nextafter(dn, 0.0)
+    for s in values:
+        if 2.0 ** -400 <= s <= 2.0 ** 400:
+            r = math.sqrt(s)
+            assert (r + s / r) / 2.0 == oracle_lib.newton_sqrt(s), s.hex()
+
+
 def test_newton_sqrt_kat():
     for x, y in golden_data.kat()["newton_sqrt"]:
         assert oracle_lib.newton_sqrt(float.fromhex(x)).hex() == float.fromhex(y).hex(), x
