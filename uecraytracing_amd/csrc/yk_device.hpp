@@ -39,9 +39,7 @@ __device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.
 // reference start everywhere (A/B timing).  The iteration bound only matters for NaN/inf.
 // YK_ABLATE (timing-only builds, tools/ablate.py; results are WRONG by design):
 //   1 = skip the MT warm-up walk, 2 = hardware sqrt instead of math::sqrt, (8: phase stamps,
-//   no change of results), 16 = no thin-lens sampling, 32 = no attenuation unwind, 64 = no
-//   colour stores, 128 = no order / x_397 loads at a sample's start, 256 = lambertian scatter
-//   vector without MT draws
+//   no change of results), 32 = no attenuation unwind, 64 = no colour stores
 #ifndef YK_ABLATE
 #define YK_ABLATE 0
 #endif

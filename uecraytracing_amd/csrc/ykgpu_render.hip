@@ -136,7 +136,8 @@ struct KernelArgs {
   uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
   uint64_t seed_key;
   const uint32_t* __restrict__ order;  // p → tile pixel (kNoPixel: empty slot of an edge block)
-  const uint32_t* __restrict__ warm;   // x_397 per sample slot of the launch
+  const uint32_t* __restrict__ warm;   // x_397 per sample slot of the launch (FP32 mt19937 kernel)
+  const void* __restrict__ start;      // StartRec per sample slot (FP64 mt19937 kernel)
   double t_min;
   double inv_w, inv_h;  // RN(1/W), RN(1/H) for the camera's exact divisions (div_markstein)
   double origin_bound;  // |o|_inf beyond which the BVH's float culling is not proven sound
@@ -279,21 +280,37 @@ __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; 
 // neighbouring pixels in both directions.  Every pixel's samples are independent of the order.
 constexpr uint32_t kNoPixel = 0xffffffffu;
 
-// Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread,
-// one 16-B store.  out[i] = x_397(seed(i)), i = (pix - pix_base) * spp + s.
+// A sample's start, precomputed by yk_mt_warmup<true> for the FP64 mt19937 kernel: the two
+// jitter canonicals (source.cpp:162-163), the accepted thin-lens point (random_in_unit_disk by
+// rejection; 0 without a lens) and the lazy cursors after those draws (x_j, x_{j+1}, x_{j+397},
+// j).  j == kNoStart: the lens loop would have reached the scratch engine's words (never seen:
+// ~55 rejections), and the render kernel starts that sample itself.
+struct alignas(16) StartRec {
+  double uc, vc, px, py;
+  uint32_t a0, a1, b, j;
+};
+static_assert(sizeof(StartRec) == 48, "StartRec layout");
+constexpr uint32_t kNoStart = 0xffffffffu;
+
+// Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread.
+// kStart = false: out[i] = x_397(seed(i)) (one 16-B store per thread; the FP32 kernel's engines);
+// kStart = true: a StartRec per sample — the walk, then the start's own draws with the lazy
+// cursors (yk_device.hpp), which thereby leave the divergent render loop.
 struct WarmArgs {
   uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode, band_log2;
   uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
+  uint32_t lens, pad_w;               // the camera has a lens (lens_radius > 0)
   uint64_t seed_key;
   const uint32_t* order;
   uint64_t n;  // sample slots in the launch
-  uint32_t* out;
+  void* out;
 };
 
+template <bool kStart>
 __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
   for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < wa.n; i0 += stride) {
-    uint32_t x[4];
+    uint32_t x[4], seed[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const uint64_t i = i0 + k < wa.n ? i0 + k : wa.n - 1;
@@ -303,13 +320,60 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       const uint32_t sm = wa.s0 + sl;
       const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh), xx = pix - tr * wa.W;
       const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
-      x[k] = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, sm);
+      x[k] = seed[k] = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, sm);
     }
     ykd::mt_walk397x4(x);
-    if (i0 + 4 <= wa.n) {
-      *(uint4*)(wa.out + i0) = make_uint4(x[0], x[1], x[2], x[3]);
+    if (!kStart) {
+      uint32_t* out = (uint32_t*)wa.out;
+      if (i0 + 4 <= wa.n) {
+        *(uint4*)(out + i0) = make_uint4(x[0], x[1], x[2], x[3]);
+      } else {
+        for (int k = 0; k < 4 && i0 + k < wa.n; ++k) out[i0 + k] = x[k];
+      }
     } else {
-      for (int k = 0; k < 4 && i0 + k < wa.n; ++k) wa.out[i0 + k] = x[k];
+      // the four samples' draws interleaved (independent cursor chains: ILP for the quarter-rate
+      // multiplies of the seeding recurrence)
+      StartRec r[4];
+      ykd::MtLane g[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        g[k].state = nullptr;
+        ykd::mt_start_from(g[k], seed[k], x[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k].uc = ykd::canonical<true>(g[k]);  // source.cpp:162: (x + dist(gen)) / W
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k].vc = ykd::canonical<true>(g[k]);  // source.cpp:163
+      uint32_t pending = 0;  // bit k: sample k still rejecting lens points
+      uint32_t failed = 0;   // bit k: the lens loop would reach the scratch engine's words
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r[k].px = r[k].py = 0.0;
+        if (wa.lens) pending |= 1u << k;
+      }
+      while (pending) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!(pending & (1u << k))) continue;
+          if (!ykd::rng_lazy_ok(g[k], 4)) {
+            failed |= 1u << k;
+            pending &= ~(1u << k);
+            continue;
+          }
+          r[k].px = ykd::uniform<true>(g[k], -1, 1);
+          r[k].py = ykd::uniform<true>(g[k], -1, 1);
+          if (r[k].px * r[k].px + r[k].py * r[k].py < 1.0) pending &= ~(1u << k);
+        }
+      }
+      StartRec* out = (StartRec*)wa.out;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r[k].a0 = g[k].a0;
+        r[k].a1 = g[k].a1;
+        r[k].b = g[k].b;
+        r[k].j = (failed & (1u << k)) ? kNoStart : g[k].j;
+        if (i0 + k < wa.n) out[i0 + k] = r[k];
+      }
     }
   }
 }
@@ -414,6 +478,11 @@ __device__ __forceinline__ void rng_start(ykd::MtLane& g, uint32_t seed, const K
 __device__ __forceinline__ void rng_start(ykd::X128Lane& g, uint32_t seed, const KernelArgs&, uint32_t) {
   ykd::x128_start(g, seed);
 }
+
+// A sample's engine from its seed alone (the FP64 kernel's start when no StartRec serves it):
+// mt19937 walks its 397 seeding steps here
+__device__ __forceinline__ void rng_start_full(ykd::MtLane& g, uint32_t seed) { ykd::mt_start(g, seed); }
+__device__ __forceinline__ void rng_start_full(ykd::X128Lane& g, uint32_t seed) { ykd::x128_start(g, seed); }
 
 __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, uint32_t lane, uint32_t& slot,
                                             uint32_t& res_base, uint32_t& res_left) {
@@ -528,43 +597,57 @@ void yk_render_persistent(KernelArgs ka) {
     uint32_t qpix = 0;
     if (start) {
       const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
-#if YK_ABLATE & 128
-      qpix = (slot - sl * ka.npix_slots) % (ka.W * ka.row_count);
-#else
       qpix = ka.order[slot - sl * ka.npix_slots];
-#endif
       start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
     if (start) {
       const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
       const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
-      // seed (uint32 wrap, source.cpp:154-158); mt19937's x_397 comes from yk_mt_warmup
-#if YK_ABLATE & 128
-      if constexpr (std::is_same<Gen, ykd::MtLane>::value)
-        ykd::mt_start_from(g, ykd::sample_seed(0u, 0, ka.seed0, y, x, ka.W, ka.spp, s), slot * 2654435761u);
-      else
-        rng_start(g, ykd::sample_seed(0u, 0, ka.seed0, y, x, ka.W, ka.spp, s), ka, slot);
-#else
-      rng_start(g, ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka,
-                slot);
-#endif
+      // seed (uint32 wrap, source.cpp:154-158)
+      const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
+      const double lens_r = ka.cam.lens_radius;
+      // The start's draws — the two jitter canonicals, then the lens point — and the engine after
+      // them: precomputed for mt19937 by yk_mt_warmup<true> (StartRec), so the divergent loop
+      // only loads them; xor128, and the (never seen) record the warm-up could not complete,
+      // draw here
+      double uc = 0, vc = 0, px = 0, py = 0;
+      bool pre = false;
+      if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
+        const StartRec r = ((const StartRec*)ka.start)[slot];
+        pre = r.j != kNoStart;
+        if (pre) {
+          g.seed = seed;
+          g.a0 = r.a0;
+          g.a1 = r.a1;
+          g.b = r.b;
+          g.j = r.j;
+          uc = r.uc;
+          vc = r.vc;
+          px = r.px;
+          py = r.py;
+        }
+      }
+      if (!pre) {
+        rng_start_full(g, seed);
+        uc = ykd::canonical<true>(g);  // (a fresh engine: its first words never need the scratch engine)
+        vc = ykd::canonical<true>(g);
+        if (lens_r > 0) {  // thin-lens extension: random_in_unit_disk by rejection
+          do {
+            px = ykd::uniform(g, -1, 1);
+            py = ykd::uniform(g, -1, 1);
+          } while (!(px * px + py * py < 1.0));
+        }
+      }
       // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
-      // (a fresh engine: its first words never need the scratch engine)
-      const double u = ykd::div_markstein((double)x + ykd::uniform<true>(g, 0, 1), (double)ka.W, ka.inv_w);
-      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform<true>(g, 0, 1), (double)ka.H, ka.inv_h);
+      const double u = ykd::div_markstein((double)x + ykd::uniform_of(uc, 0, 1), (double)ka.W, ka.inv_w);
+      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform_of(vc, 0, 1), (double)ka.H, ka.inv_h);
       // camera::get_ray (camera.hpp:29-32): llc + u*horizontal + v*vertical (- origin)
       const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
       const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
-      const double lens_r = ka.cam.lens_radius;
       d = ykd::sub(ykd::add(ykd::add(cam_llc, ykd::mul(cam_h, u)), ykd::mul(cam_v, v)), cam_o);
       o = cam_o;
-      if (!(YK_ABLATE & 16) && lens_r > 0) {  // thin-lens extension: random_in_unit_disk by rejection
-        double px, py;
-        do {
-          px = ykd::uniform(g, -1, 1);
-          py = ykd::uniform(g, -1, 1);
-        } while (!(px * px + py * py < 1.0));
+      if (lens_r > 0) {  // thin-lens offset
         const double rx = px * lens_r, ry = py * lens_r;
         const v3 lens_u = ld3(ka.cam.lens_u), lens_v = ld3(ka.cam.lens_v);
         const v3 off = ykd::add(ykd::mul(lens_u, rx), ykd::mul(lens_v, ry));
@@ -1414,7 +1497,7 @@ struct ykgpu_context {
   int cus = 0;
   DevTree t64, t32;  // the FP64 and FP32 kernels' trees over the current scene
   size_t scratch_lanes = 0;
-  uint32_t* d_warm = nullptr;  // x_397 per sample slot of one launch
+  char* d_warm = nullptr;  // warm-up ring: StartRec (FP64 mt19937) or x_397 (FP32) per sample slot
   double* d_col = nullptr;     // sample colours of one launch (kColStride doubles per slot)
   double* d_acc = nullptr;     // running per-pixel sums between launches
   size_t col_cap = 0, acc_cap = 0;
@@ -1636,9 +1719,11 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     return YK_OK;
   };
   const uint32_t nlaunch = (uint32_t)sched.size();
+  // warm-up records: the FP64 kernel's whole sample start (StartRec), the FP32 kernel's x_397
+  const size_t welem = f32 ? sizeof(uint32_t) : sizeof(StartRec);
   const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
-      nlaunch, std::max<uint64_t>(3, kWarmBytes / (4ull * nps * K)));
-  if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K, sizeof(uint32_t)))) return rc;
+      nlaunch, std::max<uint64_t>(3, kWarmBytes / (welem * nps * K)));
+  if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
   // two colour buffers: reduce c (stream red) overlaps render c + 1
   if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)2 * nps * K * kColStride, sizeof(double)))) return rc;
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
@@ -1656,7 +1741,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.nspheres = ctx->nspheres;
   ka.flags = p->flags;
   ka.id_stride = ctx->id_stride;
-  ka.warm = ctx->d_warm;
+  ka.warm = nullptr;
+  ka.start = nullptr;
   ka.order = ctx->d_order;
   ka.t_min = p->t_min;
   ka.origin_bound = tree.origin_bound;
@@ -1695,6 +1781,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.row_stride = p->row_stride;
   wa.band_log2 = p->row_band_log2;
   wa.out = ctx->d_warm;
+  wa.lens = ctx->cam.lens_radius > 0 ? 1u : 0u;
+  wa.pad_w = 0;
   wa.npix_slots = nps;
   fastdiv(nps, wa.nps_m, wa.nps_sh);
   fastdiv(p->image_width, wa.w_m, wa.w_sh);
@@ -1744,11 +1832,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
     wa.s0 = sched[c].first;
     wa.n = (uint64_t)nps * sched[c].second;
-    wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
+    wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * 32);
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
-      hipLaunchKernelGGL(yk_mt_warmup, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      if (f32)
+        hipLaunchKernelGGL(yk_mt_warmup<false>, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      else
+        hipLaunchKernelGGL(yk_mt_warmup<true>, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       YK_HIP(hipGetLastError());
     }
     YK_HIP(hipEventRecord(ev[1], ctx->aux));
@@ -1765,7 +1856,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.s0 = s0;
     ka.nsl = nsl;
     ka.col = col;
-    ka.warm = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K;
+    char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
+    ka.warm = f32 ? (const uint32_t*)wring : nullptr;
+    ka.start = f32 ? nullptr : (const void*)wring;
     // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
     // only on its own x_397 and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
