@@ -1,0 +1,398 @@
+// tools/loopsim.cpp — lockstep wave model of the FP64 kernel's traversal LOOP SHAPE, on the
+// device's own 4-wide tree (ykbvh::wide_nodes) and the kernel's visit order (last entered slot
+// next, the others pushed in slot order).  It compares loop structures by the wave-level work
+// they issue, which is what the render pays for:
+//   ifelse  — the shipped loop: per trip a lane visits an inner node OR tests a leaf;
+//   postpone — per trip a lane visits an inner node AND tests one postponed leaf (a leaf met
+//              while traversing is parked in a register and the traversal pops on).
+// Costs per wave trip are VALU-instruction weights of the blocks (measured from the ISA, command
+// line): visit, leaf discriminant, the disc >= 0 tail, loop overhead.
+//   build: g++ -O2 -std=c++17 -Iinclude tools/loopsim.cpp uecraytracing_amd/csrc/yk_bvh.cpp \
+//          uecraytracing_amd/csrc/yk_host.cpp -o /tmp/loopsim
+//   run:   /tmp/loopsim final 42 [leaf] [c_visit c_leaf c_disc c_trip]
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../include/ykgpu.h"
+#include "../uecraytracing_amd/csrc/yk_bvh.hpp"
+
+struct V {
+  double x, y, z;
+};
+static V add(V a, V b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static V sub(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static V mul(V a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+static double dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static V unit(V a) { return mul(a, 1.0 / std::sqrt(dot(a, a))); }
+static V ld(const double* p) { return {p[0], p[1], p[2]}; }
+
+constexpr int32_t kDone = INT32_MIN;  // no node (stack empty)
+constexpr int32_t kNone = 0;          // no postponed leaf (leaf codes are negative)
+
+struct Lane {
+  V o, d;
+  double a, ustar = INFINITY;
+  float ix, iy, iz, uf = INFINITY;
+  std::vector<int32_t> stk;
+  int32_t node = 0, pend = kNone;
+  bool done = false;
+};
+
+struct Model {
+  std::vector<yk_sphere> sph;
+  std::vector<ykbvh::WideNode> wide;
+  std::vector<uint32_t> order;
+  int32_t root = 0;
+
+  int hit_exact(V o, V d, double& t) const {
+    int best = -1;
+    t = INFINITY;
+    for (size_t i = 0; i < sph.size(); ++i) {
+      V oc = sub(o, ld(sph[i].center));
+      double a = dot(d, d), hb = dot(oc, d), c = dot(oc, oc) - sph[i].radius * sph[i].radius;
+      double disc = hb * hb - a * c;
+      if (disc < 0) continue;
+      double sq = std::sqrt(disc), r = (-hb - sq) / a;
+      if (r < 0.001) r = (-hb + sq) / a;
+      if (r < 0.001) continue;
+      if (r <= t) { t = r; best = (int)i; }
+    }
+    return best;
+  }
+  // one interior visit: returns the next node (or kDone after an empty pop)
+  void visit(Lane& L) const {
+    const ykbvh::WideNode& w = wide[L.node / (int32_t)sizeof(ykbvh::WideNode)];
+    const float c = 1.0f + 0x1p-17f;
+    bool hk[4];
+    for (int k = 0; k < 4; ++k) {
+      const int sx = L.ix < 0 ? 4 : 0, sy = L.iy < 0 ? 4 : 0, sz = L.iz < 0 ? 4 : 0;
+      const float nx = std::fma(w.x[sx + k], L.ix, -(float)L.o.x * L.ix);
+      const float fx = std::fma(w.x[sx + 4 + k], L.ix * c, -((float)L.o.x * L.ix * c));
+      const float ny = std::fma(w.y[sy + k], L.iy, -(float)L.o.y * L.iy);
+      const float fy = std::fma(w.y[sy + 4 + k], L.iy * c, -((float)L.o.y * L.iy * c));
+      const float nz = std::fma(w.z[sz + k], L.iz, -(float)L.o.z * L.iz);
+      const float fz = std::fma(w.z[sz + 4 + k], L.iz * c, -((float)L.o.z * L.iz * c));
+      const float tn = std::max(std::max(std::max(nx, ny), nz), 0.001f * (1 - 0x1p-17f));
+      const float tf = std::min(std::min(std::min(fx, fy), fz), L.uf);
+      hk[k] = tn <= tf;
+    }
+    int last = -1;
+    for (int k = 0; k < 4; ++k)
+      if (hk[k]) last = k;
+    if (last < 0) {
+      pop(L);
+      return;
+    }
+    for (int k = 0; k < last; ++k)
+      if (hk[k]) L.stk.push_back(w.child[k]);
+    L.node = w.child[last];
+  }
+  static void pop(Lane& L) {
+    if (L.stk.empty()) {
+      L.node = kDone;
+    } else {
+      L.node = L.stk.back();
+      L.stk.pop_back();
+    }
+  }
+  // leaf test: returns (spheres tested, disc >= 0 count)
+  std::pair<int, int> leaf(Lane& L, int32_t code) const {
+    const uint32_t v = ~(uint32_t)code, first = v >> 4, cnt = v & 15u;
+    int dpos = 0;
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const yk_sphere& s = sph[order[first + k]];
+      V oc = sub(L.o, ld(s.center));
+      double hb = dot(oc, L.d), cc = dot(oc, oc) - s.radius * s.radius;
+      double disc = hb * hb - L.a * cc;
+      if (disc < 0) continue;
+      ++dpos;
+      double sq = std::sqrt(disc), r1 = (-hb - sq) / L.a, r2 = (-hb + sq) / L.a;
+      double ub = r1 >= 0.001 ? r1 : (r2 >= 0.001 ? r2 : INFINITY);
+      if (ub < L.ustar) { L.ustar = ub; L.uf = (float)ub * (1 + 0x1p-18f); }
+    }
+    return {(int)cnt, dpos};
+  }
+};
+
+int main(int argc, char** argv) {
+  const char* scene = argc > 1 ? argv[1] : "final";
+  uint32_t seed = argc > 2 ? atoi(argv[2]) : 42;
+  ykbvh::Options opt;
+  if (argc > 3) opt.max_leaf = atoi(argv[3]);
+  const double c_visit = argc > 4 ? atof(argv[4]) : 53, c_leaf = argc > 5 ? atof(argv[5]) : 20,
+               c_disc = argc > 6 ? atof(argv[6]) : 40, c_trip = argc > 7 ? atof(argv[7]) : 10,
+               frac = argc > 8 ? atof(argv[8]) : 1.0;
+  Model M;
+  uint32_t n = 0;
+  yk_camera cam;
+  yk_scene_build(scene, seed, nullptr, 0, &n, &cam);
+  M.sph.resize(n);
+  yk_scene_build(scene, seed, M.sph.data(), n, &n, nullptr);
+  std::vector<double> c(3 * n), r(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    for (int k = 0; k < 3; ++k) c[3 * i + k] = M.sph[i].center[k];
+    r[i] = M.sph[i].radius;
+  }
+  double ext = 0;
+  for (int k = 0; k < 3; ++k) ext = std::max(ext, std::fabs(cam.origin[k]));
+  const ykbvh::Built b = ykbvh::build(c.data(), r.data(), n, ext, opt);
+  uint32_t wd = 0;
+  M.wide = ykbvh::wide_nodes(b, &M.root, &wd);
+  M.order = b.order;
+  // segment rays of a 192x108x2 path-traced image (approximate shading: the distribution matters)
+  std::mt19937_64 rng(1);
+  std::uniform_real_distribution<double> U(0, 1);
+  std::vector<std::pair<V, V>> seg;
+  const int W = 192, H = 108;
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x)
+      for (int s = 0; s < 2; ++s) {
+        double u = (x + U(rng)) / W, v = (H - y - 1 + U(rng)) / H;
+        V o = ld(cam.origin);
+        V d = sub(add(add(ld(cam.lower_left_corner), mul(ld(cam.horizontal), u)), mul(ld(cam.vertical), v)), o);
+        for (int depth = 0; depth < 50; ++depth) {
+          seg.push_back({o, d});
+          double t;
+          int id = M.hit_exact(o, d, t);
+          if (id < 0) break;
+          const yk_sphere& sp = M.sph[id];
+          V p = add(o, mul(d, t));
+          V nrm = mul(sub(p, ld(sp.center)), 1.0 / sp.radius);
+          bool front = dot(d, nrm) < 0;
+          if (!front) nrm = mul(nrm, -1);
+          if (sp.material == YK_MATERIAL_LAMBERTIAN) {
+            V q{U(rng) * 2 - 1, U(rng) * 2 - 1, U(rng) * 2 - 1};
+            d = add(nrm, unit(q));
+          } else if (sp.material == YK_MATERIAL_METAL) {
+            V ud = unit(d);
+            d = sub(ud, mul(nrm, 2 * dot(ud, nrm)));
+            if (sp.fuzz > 0) d = add(d, mul(unit(V{U(rng) - .5, U(rng) - .5, U(rng) - .5}), sp.fuzz * U(rng)));
+            if (dot(d, nrm) <= 0) break;
+          } else {
+            V ud = unit(d);
+            double ratio = front ? 1 / sp.ior : sp.ior, ct = std::min(-dot(ud, nrm), 1.0);
+            double stt = std::sqrt(1 - ct * ct);
+            if (ratio * stt > 1 || U(rng) < 0.1) d = sub(ud, mul(nrm, 2 * dot(ud, nrm)));
+            else {
+              V perp = mul(add(ud, mul(nrm, ct)), ratio);
+              d = add(perp, mul(nrm, -std::sqrt(std::fabs(1 - dot(perp, perp)))));
+            }
+          }
+          o = p;
+        }
+      }
+  std::vector<size_t> idx(seg.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+  std::shuffle(idx.begin(), idx.end(), rng);
+  auto rcp = [](float x) { return std::fabs(x) > 1e-30f ? 1.0f / x : std::copysign(1e30f, x); };
+
+  printf("%s n=%u leaf<=%u wide nodes %zu depth %u | %zu segments | weights visit %.0f leaf %.0f disc %.0f trip %.0f\n",
+         scene, n, opt.max_leaf, M.wide.size(), wd, seg.size(), c_visit, c_leaf, c_disc, c_trip);
+  // ---- wave work-pool models: one LIFO of (ray, node) pairs per wave, 64 pairs per trip
+  // pool 0: nodes and leaves mixed in the pool; pool 1: leaves go to a list tested 64 at a time
+  // (when it holds 64, or the node pool is empty)
+  for (int pv = 0; pv < 2; ++pv) {
+    double trips = 0, vis_trips = 0, leaf_trips = 0, lv = 0, ll = 0, cost = 0, maxpool = 0, ovf = 0, cand = 0;
+    std::vector<size_t> ins_hist(16, 0);
+    size_t nw = 0;
+    for (size_t g = 0; g + 64 <= idx.size(); g += 64, ++nw) {
+      std::vector<Lane> lanes(64);
+      std::vector<std::pair<int, int32_t>> pool, leaves;
+      std::vector<int> ncand(64, 0);
+      std::vector<std::vector<float>> lbs(64);
+      for (int k = 0; k < 64; ++k) {
+        Lane& L = lanes[k];
+        L.o = seg[idx[g + k]].first;
+        L.d = seg[idx[g + k]].second;
+        L.a = dot(L.d, L.d);
+        L.ix = rcp((float)L.d.x), L.iy = rcp((float)L.d.y), L.iz = rcp((float)L.d.z);
+        pool.push_back({k, M.root});
+      }
+      auto leaf_test = [&](int k, int32_t code) {
+        Lane& L = lanes[k];
+        const uint32_t v = ~(uint32_t)code, first = v >> 4, cnt = v & 15u;
+        for (uint32_t q = 0; q < cnt; ++q) {
+          const yk_sphere& s = M.sph[M.order[first + q]];
+          V oc = sub(L.o, ld(s.center));
+          double hb = dot(oc, L.d), cc = dot(oc, oc) - s.radius * s.radius;
+          double disc = hb * hb - L.a * cc;
+          ++ll;
+          if (disc < 0) continue;
+          double sq = std::sqrt(disc), r1 = (-hb - sq) / L.a, r2 = (-hb + sq) / L.a;
+          double lb = r1 >= 0.001 ? r1 : r2;
+          double ub = r1 >= 0.001 ? r1 : (r2 >= 0.001 ? r2 : INFINITY);
+          if (!(lb <= L.ustar)) continue;
+          if (ub < L.ustar) { L.ustar = ub; L.uf = (float)ub * (1 + 0x1p-18f); }
+          lbs[k].push_back((float)lb);
+        }
+      };
+      while (!pool.empty() || !leaves.empty()) {
+        std::vector<std::pair<int, int32_t>> take;
+        bool leaf_trip = false;
+        if (pv == 1 && (leaves.size() >= 64 || pool.empty())) {
+          const size_t n = std::min<size_t>(64, leaves.size());
+          take.assign(leaves.end() - n, leaves.end());
+          leaves.resize(leaves.size() - n);
+          leaf_trip = true;
+        } else {
+          const size_t n = std::min<size_t>(64, pool.size());
+          take.assign(pool.end() - n, pool.end());
+          pool.resize(pool.size() - n);
+        }
+        // snapshot of U* at the trip's start (updates land after the trip)
+        std::vector<float> uf(64);
+        for (int k = 0; k < 64; ++k) uf[k] = lanes[k].uf;
+        bool any_v = false, any_l = false;
+        std::vector<std::pair<int, int32_t>> pushed;
+        for (auto [k, code] : take) {
+          if (code >= 0) {
+            any_v = true;
+            ++lv;
+            Lane L = lanes[k];
+            L.uf = uf[k];
+            L.stk.clear();
+            L.node = code;
+            M.visit(L);
+            // children entered: the stack (in push order) plus the next node
+            for (int32_t c : L.stk) pushed.push_back({k, c});
+            if (L.node != kDone) pushed.push_back({k, L.node});
+          } else if (code != ykbvh::kEmptyLeaf) {
+            any_l = true;
+            leaf_test(k, code);
+          }
+        }
+        for (auto& e : pushed) {
+          if (pv == 1 && e.second < 0) leaves.push_back(e);
+          else pool.push_back(e);
+        }
+        maxpool = std::max(maxpool, (double)(pool.size() + leaves.size()));
+        trips += 1;
+        vis_trips += any_v;
+        leaf_trips += any_l;
+        cost += c_trip + (any_v ? c_visit + 25 : 0) + (any_l ? c_leaf + c_disc + 25 : 0);
+      }
+      for (int k = 0; k < 64; ++k) {
+        int n = 0;
+        for (float lb : lbs[k]) n += lb <= lanes[k].uf;
+        cand += n;
+        ovf += lbs[k].size() > 4;
+        ins_hist[std::min<size_t>(lbs[k].size(), 15)]++;
+      }
+    }
+    printf("pool %d: per wave-segment: trips %.1f (visit %.1f, leaf %.1f) | per lane: visits %.2f leaf tests %.2f, "
+           "final candidates %.2f, inserted > 4: %.5f | max pool %.0f | cost %.0f\n",
+           pv, trips / nw, vis_trips / nw, leaf_trips / nw, lv / (64.0 * nw), ll / (64.0 * nw), cand / (64.0 * nw),
+           ovf / (64.0 * nw), maxpool, cost / nw);
+    printf("  inserted candidates per ray:");
+    for (int q = 0; q < 16; ++q) printf(" [%d]%zu", q, ins_hist[q]);
+    printf("\n");
+  }
+  for (int variant = 0; variant < 4; ++variant) {
+    double trips = 0, wv = 0, wl = 0, wd2 = 0, lv = 0, ll = 0, cost = 0;
+    size_t nw = 0;
+    for (size_t g = 0; g + 64 <= idx.size(); g += 64, ++nw) {
+      std::vector<Lane> lanes(64);
+      for (int k = 0; k < 64; ++k) {
+        Lane& L = lanes[k];
+        L.o = seg[idx[g + k]].first;
+        L.d = seg[idx[g + k]].second;
+        L.a = dot(L.d, L.d);
+        L.ix = rcp((float)L.d.x), L.iy = rcp((float)L.d.y), L.iz = rcp((float)L.d.z);
+        L.node = M.root;
+      }
+      for (;;) {
+        bool any_v = false, any_l = false;
+        int max_cnt = 0, max_dpos = 0, act = 0;
+        // variant 3 (Aila-Laine speculative): leaves are tested only when every active lane has
+        // one parked or nothing left to visit
+        bool test_now = true;
+        if (variant == 3) {
+          int ready = 0, live = 0;
+          for (auto& L : lanes)
+            if (!L.done) {
+              ++live;
+              ready += !(L.pend == kNone && L.node != kDone);
+            }
+          test_now = ready >= frac * live;
+        }
+        for (auto& L : lanes) {
+          if (L.done) continue;
+          ++act;
+          if (variant == 3) {
+            if (test_now && L.pend != kNone) {
+              any_l = true;
+              auto [cnt, dp] = M.leaf(L, L.pend);
+              ll += cnt;
+              max_cnt = std::max(max_cnt, cnt);
+              max_dpos = std::max(max_dpos, dp);
+              L.pend = kNone;
+            }
+            if (L.node >= 0) {
+              any_v = true;
+              ++lv;
+              M.visit(L);
+            }
+            if (L.pend == kNone && L.node != kDone && L.node < 0) {
+              L.pend = L.node;
+              M.pop(L);
+            }
+            if (L.node == kDone && L.pend == kNone) L.done = true;
+          } else if (variant == 0) {  // ifelse
+            if (L.node >= 0) {
+              any_v = true;
+              ++lv;
+              M.visit(L);
+              if (L.node == kDone) L.done = true;
+            } else {
+              any_l = true;
+              auto [cnt, dp] = M.leaf(L, L.node);
+              ll += cnt;
+              max_cnt = std::max(max_cnt, cnt);
+              max_dpos = std::max(max_dpos, dp);
+              M.pop(L);
+              if (L.node == kDone) L.done = true;
+            }
+          } else {  // postpone (variant 2: the leaf test before the visit)
+            auto do_leaf = [&]() {
+              if (L.pend != kNone) {
+                any_l = true;
+                auto [cnt, dp] = M.leaf(L, L.pend);
+                ll += cnt;
+                max_cnt = std::max(max_cnt, cnt);
+                max_dpos = std::max(max_dpos, dp);
+                L.pend = kNone;
+              }
+            };
+            if (variant == 2) do_leaf();
+            if (L.node >= 0) {
+              any_v = true;
+              ++lv;
+              M.visit(L);
+            }
+            if (L.pend == kNone && L.node != kDone && L.node < 0) {
+              L.pend = L.node;
+              M.pop(L);
+            }
+            if (variant == 1) do_leaf();
+            if (L.node == kDone && L.pend == kNone) L.done = true;
+          }
+        }
+        if (!act) break;
+        trips += 1;
+        wv += any_v;
+        wl += max_cnt;
+        wd2 += max_dpos;
+        cost += c_trip + c_visit * any_v + c_leaf * max_cnt + c_disc * max_dpos;
+      }
+    }
+    const char* name[4] = {"ifelse", "postpone(visit,leaf)", "postpone(leaf,visit)", "speculative"};
+    printf("%-22s per wave-segment: trips %.1f, visit blocks %.1f, leaf iters %.1f, disc tails %.1f | "
+           "per lane: visits %.2f leaf tests %.2f | cost %.0f\n",
+           name[variant], trips / nw, wv / nw, wl / nw, wd2 / nw, lv / (64.0 * nw), ll / (64.0 * nw), cost / nw);
+  }
+  return 0;
+}

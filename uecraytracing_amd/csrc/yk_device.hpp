@@ -248,19 +248,21 @@ __device__ __forceinline__ void mt_start_from(MtLane& g, uint32_t seed, uint32_t
   g.b = x397;
 }
 
-// x_397 of the seeding sequence (random.hpp:69-81) for four seeds at once (independent chains
+// x_397 of the seeding sequence (random.hpp:69-81) for N seeds at once (independent chains
 // interleaved for ILP).  Under YK_ABLATE & 1 the walk is skipped (timing-only builds).
-__device__ __forceinline__ void mt_walk397x4(uint32_t (&x)[4]) {
+template <int N>
+__device__ __forceinline__ void mt_walk397xn(uint32_t (&x)[N]) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) x[k] = mt_seed_step(x[k], 1);
+  for (int k = 0; k < N; ++k) x[k] = mt_seed_step(x[k], 1);
 #if !(YK_ABLATE & 1)
 #pragma unroll 4
   for (uint32_t i = 2; i <= kMtM; ++i) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = mt_seed_step(x[k], i);
+    for (int k = 0; k < N; ++k) x[k] = mt_seed_step(x[k], i);
   }
 #endif
 }
+__device__ __forceinline__ void mt_walk397x4(uint32_t (&x)[4]) { mt_walk397xn<4>(x); }
 
 // The rare path: the real engine in global scratch (seed :69-81, M_gen_rand :114-131).
 // Out of line and by value so the hot path keeps the lane's cursors in registers.

@@ -6,10 +6,12 @@
 //
 // Execution model:
 //   * a render call is a sequence of LAUNCHES of K samples per pixel (8, 32, then at most
-//     kLaunchSpp = 64; 1920x1080x512: 8, 32, 7 x 64, 24).  Per launch: yk_mt_warmup (x_397 of every sample's mt19937 seeding
-//     sequence, second stream), yk_render_persistent (the paths), yk_reduce_samples (the
+//     kLaunchSpp = 64; 1920x1080x512: 8, 32, 7 x 64, 24).  Per launch: yk_mt_warmup (second
+//     stream: every sample's mt19937 seeding walk and, for the FP64 kernel, its start draws —
+//     jitter and lens — as a StartRec), yk_render_persistent (the paths), yk_reduce_samples (the
 //     reference's strictly sequential per-pixel sum and to_color3b, third stream).
-//   * yk_render_persistent is one persistent grid over SAMPLE SLOTS: a lane runs one path at a
+//   * yk_render_persistent is one persistent grid of 768-thread workgroups, one per CU, with
+//     the scene (BVH, geometry and material tables) in LDS, over SAMPLE SLOTS: a lane runs one path at a
 //     time, one SEGMENT (closest hit + scatter) per trip round the loop, writes the sample's
 //     colour when the path ends and takes the next slot from a wave-level reserve (one atomic
 //     per 512 slots) — active-lane refill, so no lane idles while the launch has slots.
@@ -20,6 +22,9 @@
 //   * closest hit: a 4-wide BVH in LDS culls conservatively in float, the candidates' roots
 //     are evaluated with the reference's exact arithmetic, ties to the later tuple index
 //      — the result equals the reference's ordered scan bit for bit.
+//   * every operation several lane kinds need runs once per trip for all of them (shared
+//     canonical block, normalisation and second square root in shading): a wave pays for each
+//     branch any of its lanes takes ("Uniform work per trip").
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -73,7 +78,11 @@ static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 
 // One 768-thread workgroup per CU (12 waves, 3 per SIMD): the scene is copied into LDS once per
 // CU instead of once per 256-thread block, which leaves room for the shading tables (sphere
-// geometry and materials in tuple order) beside the BVH and full-depth traversal stacks
+// geometry and materials in tuple order) beside the BVH and the traversal stacks.  The fourth
+// wave slot of each SIMD (128 of its 512 VGPRs) is left to the yk_mt_warmup waves, which run the
+// next launch's seed walks in the render's idle issue cycles.  (1024 threads, 4 render waves per
+// SIMD: the node loop is bound by LDS latency, so the render alone runs 4% faster — 184 vs 192 ms
+// per 512-spp frame without the walks — but the walks can no longer overlap: 218 vs 215 ms.)
 #ifndef YK_BLOCK
 #define YK_BLOCK 768
 #endif
@@ -92,6 +101,17 @@ constexpr int kBlock = YK_BLOCK;
 using DevNode = ykbvh::WideNode;
 #else
 using DevNode = ykbvh::SlabNode;
+#endif
+// YK_SPEC_LEAF (4-wide trees): speculative traversal.  A lane that reaches a leaf parks it and
+// traverses on; the wave tests parked leaves together, once at least YK_SPEC_LEAF/16 of its
+// traversing lanes hold one (16: all).  0 = the if/else loop (a lane visits OR tests per trip).
+#ifndef YK_SPEC_LEAF
+#define YK_SPEC_LEAF 0
+#endif
+// YK_CAND_COMPACT: the exact roots of the traversal's surviving candidates are evaluated as one
+// wave-wide list (lane j of the wave evaluates list entry j), not as up to four per-lane blocks
+#ifndef YK_CAND_COMPACT
+#define YK_CAND_COMPACT 0
 #endif
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (diagnostic builds), [24..31]: work
 
@@ -273,6 +293,28 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
   }
 }
 
+// The same root for the compacted evaluation (YK_CAND_COMPACT): the accepted root of sphere i, or
+// NaN when neither root reaches t_min (a NaN passes neither comparison of the closest-hit rule,
+// so the owner's merge skips it; an infinite root is kept and compared as in exact_candidate).
+// Work counters go to `cnt`.
+__device__ __forceinline__ double candidate_root(const SphereGeo* __restrict__ geo, uint32_t i, v3 o, v3 d,
+                                                 double a, double ra, bool a_ok, double tmin, Hit& cnt) {
+  const SphereGeo sg = geo[i];
+  const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
+  const double hb = ykd::dot(oc, d);
+  const double c = ykd::len2(oc) - sg.rr;
+  const double disc = hb * hb - a * c;
+  if (disc < 0) return __builtin_nan("");  // never taken: the candidate passed the same test
+  ++cnt.sqrts;
+  const double sq = ykd::nsqrt_c(disc, cnt.ncalls, cnt.nits);
+  double r = root_div(-hb - sq, a, ra, a_ok);
+  if (r < tmin) {
+    r = root_div(-hb + sq, a, ra, a_ok);
+    if (r < tmin) return __builtin_nan("");
+  }
+  return r;
+}
+
 __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
 
 // Processing order: slot p of a call renders tile pixel order[p] (ykgpu_context::order, built on
@@ -306,13 +348,17 @@ struct WarmArgs {
   void* out;
 };
 
+#ifndef YK_WARM_K
+#define YK_WARM_K 4
+#endif
 template <bool kStart>
 __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
-  for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < wa.n; i0 += stride) {
-    uint32_t x[4], seed[4];
+  constexpr int K = kStart ? YK_WARM_K : 4;  // samples per thread, interleaved
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * K;
+  for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * K; i0 < wa.n; i0 += stride) {
+    uint32_t x[K], seed[K];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < K; ++k) {
       const uint64_t i = i0 + k < wa.n ? i0 + k : wa.n - 1;
       const uint32_t sl = fdiv((uint32_t)i, wa.nps_m, wa.nps_sh), pp = (uint32_t)i - sl * wa.npix_slots;
       const uint32_t q = wa.order[pp];
@@ -322,8 +368,8 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
       x[k] = seed[k] = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, sm);
     }
-    ykd::mt_walk397x4(x);
-    if (!kStart) {
+    ykd::mt_walk397xn<K>(x);
+    if constexpr (!kStart) {
       uint32_t* out = (uint32_t*)wa.out;
       if (i0 + 4 <= wa.n) {
         *(uint4*)(out + i0) = make_uint4(x[0], x[1], x[2], x[3]);
@@ -333,27 +379,27 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
     } else {
       // the four samples' draws interleaved (independent cursor chains: ILP for the quarter-rate
       // multiplies of the seeding recurrence)
-      StartRec r[4];
-      ykd::MtLane g[4];
+      StartRec r[K];
+      ykd::MtLane g[K];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < K; ++k) {
         g[k].state = nullptr;
         ykd::mt_start_from(g[k], seed[k], x[k]);
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) r[k].uc = ykd::canonical<true>(g[k]);  // source.cpp:162: (x + dist(gen)) / W
+      for (int k = 0; k < K; ++k) r[k].uc = ykd::canonical<true>(g[k]);  // source.cpp:162: (x + dist(gen)) / W
 #pragma unroll
-      for (int k = 0; k < 4; ++k) r[k].vc = ykd::canonical<true>(g[k]);  // source.cpp:163
+      for (int k = 0; k < K; ++k) r[k].vc = ykd::canonical<true>(g[k]);  // source.cpp:163
       uint32_t pending = 0;  // bit k: sample k still rejecting lens points
       uint32_t failed = 0;   // bit k: the lens loop would reach the scratch engine's words
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < K; ++k) {
         r[k].px = r[k].py = 0.0;
         if (wa.lens) pending |= 1u << k;
       }
       while (pending) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < K; ++k) {
           if (!(pending & (1u << k))) continue;
           if (!ykd::rng_lazy_ok(g[k], 4)) {
             failed |= 1u << k;
@@ -367,7 +413,7 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       }
       StartRec* out = (StartRec*)wa.out;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < K; ++k) {
         r[k].a0 = g[k].a0;
         r[k].a1 = g[k].a1;
         r[k].b = g[k].b;
@@ -517,6 +563,9 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
 // instance 0.6% through SGPR spills); bit 2: the yk::xor128 engine (YK_RNG_XOR128)
 template <bool kSceneInLds, int kMode>
 __global__ __launch_bounds__(kBlock)
+#ifdef YK_RENDER_VGPRS
+__attribute__((amdgpu_num_vgpr(YK_RENDER_VGPRS)))
+#endif
 #if YK_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
 #endif
@@ -731,6 +780,16 @@ void yk_render_persistent(KernelArgs ka) {
 #else
         uint32_t sp = 0;
 #endif
+#if YK_WIDE && YK_SPEC_LEAF
+        int32_t pend = ykbvh::kEmptyLeaf;  // the parked leaf (kEmptyLeaf: none)
+#define YK_POP_NODE()          \
+  if (top == stk) {            \
+    node = ykbvh::kEmptyLeaf;  \
+  } else {                     \
+    top -= kBlock;             \
+    node = *top;               \
+  }
+#endif
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
@@ -783,8 +842,15 @@ void yk_render_persistent(KernelArgs ka) {
                 top = stk;
                 node = ykbvh::kEmptyLeaf;
               }
+#if !YK_SPEC_LEAF
               continue;
+#endif
             }
+#if YK_SPEC_LEAF
+            else {
+              YK_POP_NODE();
+            }
+#endif
 #else
             // near / far distances of both children per axis, one packed FMA per pair:
             // t = plane*(1/d) - o*(1/d)
@@ -817,9 +883,26 @@ void yk_render_persistent(KernelArgs ka) {
               continue;
             }
 #endif
-          } else {
+          }
+#if YK_WIDE && YK_SPEC_LEAF
+          // park a leaf reached while none is parked, and traverse on
+          if (node < 0 && node != ykbvh::kEmptyLeaf && pend == ykbvh::kEmptyLeaf) {
+            pend = node;
+            YK_POP_NODE();
+          }
+          // test the parked leaves together once enough lanes hold one (a finished lane counts
+          // as ready): a wave-uniform branch, skipped on the other trips (an empty parked slot
+          // is the empty leaf: no spheres)
+          const bool ready = pend != ykbvh::kEmptyLeaf || node == ykbvh::kEmptyLeaf;
+          if (__builtin_popcountll(__ballot(ready)) * 16 >= __builtin_popcountll(__ballot(1)) * YK_SPEC_LEAF) {
+            const int32_t leaf = pend;
+            pend = ykbvh::kEmptyLeaf;
+#else
+          else {
+            const int32_t leaf = node;
+#endif
             YK_STAMP(2);  // interior nodes since the last stamp
-            const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
+            const uint32_t v = ~(uint32_t)leaf, first = v >> 4, cnt = v & 15u;
 #ifdef YK_LEAF_UNROLL
 #pragma unroll YK_LEAF_UNROLL
 #endif
@@ -868,7 +951,10 @@ void yk_render_persistent(KernelArgs ka) {
             }
             YK_STAMP(6);  // this leaf
           }
-#if YK_WIDE
+#if YK_WIDE && YK_SPEC_LEAF
+          if (node == ykbvh::kEmptyLeaf && pend == ykbvh::kEmptyLeaf) break;
+#undef YK_POP_NODE
+#elif YK_WIDE
           if (top == stk) break;
           top -= kBlock;
           node = *top;
@@ -882,14 +968,72 @@ void yk_render_persistent(KernelArgs ka) {
         if (overflow) {
           linear = true;
         } else {
-          // exact evaluation of the survivors, all lanes in step; the roots' divisor a is the
-          // same for every candidate, so its refined reciprocal is computed once
+          // exact evaluation of the survivors; the roots' divisor a is the same for every
+          // candidate of a ray, so its refined reciprocal is computed once
           const bool a_ok = ykd::div_range(a);
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
+#if YK_CAND_COMPACT
+          // As one wave-wide list: most lanes hold one candidate, a few up to four, and per-lane
+          // blocks would run max-over-lanes times.  The owners post (sphere id, owner lane) at list
+          // positions from ballot prefix counts; every lane of the branch evaluates entries
+          // rank, rank + n, ... with the owner's ray fetched by lane shuffles; the roots come back
+          // through LDS and each owner merges its own under the closest-hit rule, which is a min
+          // with ties to the larger id (order-free).  The list lives in this wave's columns of the
+          // traversal stacks, free again now: ids in rows 0-3, roots (f64) in rows 4-11
+          // (stack_entries >= 12, upload_tree).
+          {
+            const bool e0 = nc > 0 && l0 <= ustar_f, e1 = nc > 1 && l1 <= ustar_f;
+            const bool e2 = nc > 2 && l2 <= ustar_f, e3 = nc > 3 && l3 <= ustar_f;
+            const uint64_t below = (1ull << lane) - 1ull;
+            const uint64_t m0 = __ballot(e0), m1 = __ballot(e1), m2 = __ballot(e2), m3 = __ballot(e3);
+            const uint32_t p1 = __popcll(m0), p2 = p1 + __popcll(m1), p3 = p2 + __popcll(m2);
+            const uint32_t total = p3 + __popcll(m3);
+            uint32_t* const wcol = (uint32_t*)stk - lane;  // this wave's column 0, row 0
+            const uint32_t g0 = __popcll(m0 & below), g1 = p1 + __popcll(m1 & below);
+            const uint32_t g2 = p2 + __popcll(m2 & below), g3 = p3 + __popcll(m3 & below);
+            const uint32_t tag = lane << 16;
+            if (e0) wcol[(g0 >> 6) * kBlock + (g0 & 63u)] = c0 | tag;
+            if (e1) wcol[(g1 >> 6) * kBlock + (g1 & 63u)] = c1 | tag;
+            if (e2) wcol[(g2 >> 6) * kBlock + (g2 & 63u)] = c2 | tag;
+            if (e3) wcol[(g3 >> 6) * kBlock + (g3 & 63u)] = c3 | tag;
+            auto root_at = [&](uint32_t g) -> double* {
+              return (double*)(wcol + (4u + (g >> 5)) * kBlock) + (g & 31u);
+            };
+            const uint64_t act = __ballot(1);
+            const uint32_t nact = __popcll(act), rank = __popcll(act & below);
+            for (uint32_t base = 0; base < total; base += nact) {  // wave-uniform
+              const uint32_t g = base + rank;
+              const bool mine = g < total;
+              const uint32_t w = mine ? wcol[(g >> 6) * kBlock + (g & 63u)] : lane << 16;
+              const int src = (int)(w >> 16);
+              // the owner's ray: every lane of the branch takes part in the shuffles
+              const v3 wo = {__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src)};
+              const v3 wd = {__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src)};
+              const double wa = __shfl(a, src), wra = __shfl(ra, src);
+              if (mine) {
+                *root_at(g) = candidate_root(geo, w & 0xffffu, wo, wd, wa, wra, ykd::div_range(wa), ka.t_min, hit);
+              }
+            }
+            // closest wins; an exact tie goes to the later tuple index (hittable_list.hpp:36-43)
+            auto merge = [&](bool e, uint32_t g, uint32_t id) {
+              if (!e) return;
+              const double r = *root_at(g);
+              if (r < hit.T || (r == hit.T && (int)id > hit.hid)) {
+                hit.T = r;
+                hit.hid = (int)id;
+              }
+            };
+            merge(e0, g0, c0);
+            merge(e1, g1, c1);
+            merge(e2, g2, c2);
+            merge(e3, g3, c3);
+          }
+#else
           if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 1 && l1 <= ustar_f) exact_candidate(geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 2 && l2 <= ustar_f) exact_candidate(geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 3 && l3 <= ustar_f) exact_candidate(geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
+#endif
         }
       }
       if (linear) {
@@ -1692,8 +1836,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
   const uint32_t spp = p->samples_per_pixel;
   // (slots of a launch stay below 2^31: the kernels' fdiv takes 31-bit numerators)
+  // A launch of few pixels still gets enough slots to fill the persistent grid (16 per lane):
+  // a thin row tile at high spp would otherwise run dozens of launches that each pay a ramp and
+  // a drain.  Neither floor nor cap exceeds the colour budget or 2^31 slots.
+  const uint64_t fill_spp = ((uint64_t)grid * kBlock * 16 + nps - 1) / nps;
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>({spp, kColourBytes / (8ull * kColStride * nps), kLaunchSpp, ((1ull << 31) - 1) / nps}));
+      1, std::min<uint64_t>({spp, kColourBytes / (8ull * kColStride * nps), std::max<uint64_t>(kLaunchSpp, fill_spp),
+                             ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
   for (uint32_t s0 = 0, k = std::min(kFirstLaunch, kmax); s0 < spp;) {
     uint32_t take = std::min(k, spp - s0);
@@ -1985,9 +2134,10 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   const size_t scene_bytes = a16(t.n_nodes * sizeof(DevNode)) + a16(count * elem) + a16(count * sizeof(uint32_t));
   const size_t tgeo_bytes = table_bytes ? a16(count * sizeof(SphereGeo)) : 0;
   const size_t mat_bytes = table_bytes ? a16(count * sizeof(SphereMat)) : 0;
-  // a CU holds 768 / kBlock workgroups (3 waves per SIMD); 2 KB below the share: the hardware's
-  // allocation granularity (3 blocks of 54144 bytes measured only 2 resident per CU)
-  const size_t budget = (size_t)160 * 1024 / std::max(1, 768 / kBlock) - 2048;
+  // a CU holds one workgroup of >= 768 threads (768 / kBlock of smaller ones); 2 KB below the
+  // share: the hardware's allocation granularity (3 blocks of 54144 bytes measured only 2
+  // resident per CU)
+  const size_t budget = (size_t)160 * 1024 / (kBlock >= 768 ? 1 : 768 / kBlock) - 2048;
   const size_t min_stacks = (size_t)12 * kBlock * 4;
   t.in_lds = scene_bytes + tgeo_bytes + mat_bytes + min_stacks <= budget;
   const size_t tables = t.in_lds ? tgeo_bytes + mat_bytes : 0;
@@ -2148,12 +2298,19 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   }
   double cam_ext = 0;
   for (int k = 0; k < 3; ++k) cam_ext = std::max(cam_ext, std::fabs(camera->origin[k]));
+  // one sphere per leaf for the 4-wide FP64 tree: 64-spp A/B on the final scene 32.5 -> 31.7 ms
+  // against two (three: 33.4); YKGPU_BVH_LEAF / YKGPU_BVH_LEAF_F32 override for A/B runs
+  auto leaf_env = [](const char* name, uint32_t def) -> uint32_t {
+    const char* e = std::getenv(name);
+    return e ? (uint32_t)std::max(1, std::min(15, std::atoi(e))) : def;
+  };
   ykbvh::Options bopt;
-  if (const char* e = std::getenv("YKGPU_BVH_LEAF")) bopt.max_leaf = std::max(1, std::min(15, std::atoi(e)));
+  bopt.max_leaf = leaf_env("YKGPU_BVH_LEAF", 1);
   int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, geo.data(), sizeof(SphereGeo),
                        sizeof(SphereGeo) + sizeof(SphereMat), fp64_kernel(true, 0), fp64_kernel(false, 0));
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
+  fopt.max_leaf = leaf_env("YKGPU_BVH_LEAF_F32", 2);
   fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
   fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
   rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4), 0,
