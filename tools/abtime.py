@@ -1,8 +1,8 @@
 """A/B wall time of library variants on the headline workload at a chosen spp (production
 instance, flags=0): one subprocess per variant run (one library per process), interleaved.
 usage: python tools/abtime.py <spp> <variant> [<variant> ...]   (variant 'base' = lib/libykgpu.so,
-otherwise lib/abl/libykgpu_<variant>.so; "<variant>@VAR=value" also sets an environment variable
-of that run, e.g. base@YKGPU_BVH_LEAF=1); AB_ROWS="begin:count:stride" renders a row tile only
+otherwise lib/abl/libykgpu_<variant>.so; "<variant>@VAR=value[@VAR2=value2...]" also sets
+environment variables of that run, e.g. base@YKGPU_BVH_LEAF=1); AB_ROWS="begin:count:stride" renders a row tile only
 (e.g. "0:135:8" = rank 0 of 8); AB_PREC=1 times the FP32 mode"""
 import json
 import os
@@ -32,11 +32,11 @@ reps = os.environ.get("AB_REPS", "3")
 names = sys.argv[2:] or ["base"]
 for rnd in range(2):
     for name in names:
-        lname, _, envspec = name.partition("@")
+        lname, *envspecs = name.split("@")
         lib = os.path.join(ROOT, "uecraytracing_amd/lib/libykgpu.so") if lname == "base" else \
             os.path.join(ROOT, f"uecraytracing_amd/lib/abl/libykgpu_{lname}.so")
         env = dict(os.environ, YKGPU_LIB_OVERRIDE=lib)
-        if envspec:
+        for envspec in envspecs:
             k, _, v = envspec.partition("=")
             env[k] = v
         out = subprocess.run([sys.executable, "-c", CODE, spp, reps, os.environ.get("AB_ROWS", ""),

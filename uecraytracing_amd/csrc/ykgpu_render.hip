@@ -102,17 +102,6 @@ using DevNode = ykbvh::WideNode;
 #else
 using DevNode = ykbvh::SlabNode;
 #endif
-// YK_SPEC_LEAF (4-wide trees): speculative traversal.  A lane that reaches a leaf parks it and
-// traverses on; the wave tests parked leaves together, once at least YK_SPEC_LEAF/16 of its
-// traversing lanes hold one (16: all).  0 = the if/else loop (a lane visits OR tests per trip).
-#ifndef YK_SPEC_LEAF
-#define YK_SPEC_LEAF 0
-#endif
-// YK_CAND_COMPACT: the exact roots of the traversal's surviving candidates are evaluated as one
-// wave-wide list (lane j of the wave evaluates list entry j), not as up to four per-lane blocks
-#ifndef YK_CAND_COMPACT
-#define YK_CAND_COMPACT 0
-#endif
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (diagnostic builds), [24..31]: work
 
 // Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
@@ -293,28 +282,6 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
   }
 }
 
-// The same root for the compacted evaluation (YK_CAND_COMPACT): the accepted root of sphere i, or
-// NaN when neither root reaches t_min (a NaN passes neither comparison of the closest-hit rule,
-// so the owner's merge skips it; an infinite root is kept and compared as in exact_candidate).
-// Work counters go to `cnt`.
-__device__ __forceinline__ double candidate_root(const SphereGeo* __restrict__ geo, uint32_t i, v3 o, v3 d,
-                                                 double a, double ra, bool a_ok, double tmin, Hit& cnt) {
-  const SphereGeo sg = geo[i];
-  const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
-  const double hb = ykd::dot(oc, d);
-  const double c = ykd::len2(oc) - sg.rr;
-  const double disc = hb * hb - a * c;
-  if (disc < 0) return __builtin_nan("");  // never taken: the candidate passed the same test
-  ++cnt.sqrts;
-  const double sq = ykd::nsqrt_c(disc, cnt.ncalls, cnt.nits);
-  double r = root_div(-hb - sq, a, ra, a_ok);
-  if (r < tmin) {
-    r = root_div(-hb + sq, a, ra, a_ok);
-    if (r < tmin) return __builtin_nan("");
-  }
-  return r;
-}
-
 __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; }
 
 // Processing order: slot p of a call renders tile pixel order[p] (ykgpu_context::order, built on
@@ -322,7 +289,7 @@ __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; 
 // neighbouring pixels in both directions.  Every pixel's samples are independent of the order.
 constexpr uint32_t kNoPixel = 0xffffffffu;
 
-// A sample's start, precomputed by yk_mt_warmup<true> for the FP64 mt19937 kernel: the two
+// A sample's start, precomputed by yk_mt_warmup<true, lens> for the FP64 mt19937 kernel: the two
 // jitter canonicals (source.cpp:162-163), the accepted thin-lens point (random_in_unit_disk by
 // rejection; 0 without a lens) and the lazy cursors after those draws (x_j, x_{j+1}, x_{j+397},
 // j).  j == kNoStart: the lens loop would have reached the scratch engine's words (never seen:
@@ -334,10 +301,14 @@ struct alignas(16) StartRec {
 static_assert(sizeof(StartRec) == 48, "StartRec layout");
 constexpr uint32_t kNoStart = 0xffffffffu;
 
-// Seed walk of every sample of a launch, fully coherent: four consecutive samples per thread.
-// kStart = false: out[i] = x_397(seed(i)) (one 16-B store per thread; the FP32 kernel's engines);
-// kStart = true: a StartRec per sample — the walk, then the start's own draws with the lazy
-// cursors (yk_device.hpp), which thereby leave the divergent render loop.
+// Seed walk of every sample of a launch, fully coherent: K consecutive samples per thread.
+// kStart = false: out[i] = x_397(seed(i)) (four samples per thread, one 16-B store; the FP32
+// kernel's engines); kStart = true: a StartRec per sample — the walk, then the start's own draws
+// with the lazy cursors (yk_device.hpp), which thereby leave the divergent render loop; kLens:
+// the camera has a lens (the rejection loop is compiled only then: its registers cost
+// co-resident waves).  The walk is ~400 dependent steps of xor-shift, v_mul_lo_u32 and add per
+// sample (8.9e12 steps/s on the whole GPU, tools/walkbench.hip: 47 ms of a 512-spp frame if it
+// ran alone), so these waves live on the render's idle issue cycles at lower priority.
 struct WarmArgs {
   uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode, band_log2;
   uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
@@ -348,10 +319,13 @@ struct WarmArgs {
   void* out;
 };
 
+// YK_WARM_K samples per thread, interleaved.  One: the StartRec kernel then needs 26 VGPRs (30
+// with a lens), so four of its waves fit beside the three render waves of each SIMD (512-spp A/B:
+// 4 -> 215.5 ms, 2 -> 211.2, 1 -> 204.6; with the render at 128 VGPRs, 1 -> 202.4)
 #ifndef YK_WARM_K
-#define YK_WARM_K 4
+#define YK_WARM_K 1
 #endif
-template <bool kStart>
+template <bool kStart, bool kLens>
 __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
   constexpr int K = kStart ? YK_WARM_K : 4;  // samples per thread, interleaved
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * K;
@@ -395,7 +369,7 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         r[k].px = r[k].py = 0.0;
-        if (wa.lens) pending |= 1u << k;
+        if (kLens) pending |= 1u << k;
       }
       while (pending) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
 #pragma unroll
@@ -460,9 +434,7 @@ struct ReduceArgs {
   uint32_t npix_slots, nsl, ks, spp;
   uint32_t first, last, pad0, pad1;
 };
-__global__ __launch_bounds__(256) void yk_reduce_samples(ReduceArgs ra) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= ra.npix_slots) return;
+__device__ __forceinline__ void reduce_slot(const ReduceArgs& ra, uint32_t p) {
   const uint32_t q = ra.order[p];
   if (q == kNoPixel) return;
   double a[3];
@@ -487,6 +459,10 @@ __global__ __launch_bounds__(256) void yk_reduce_samples(ReduceArgs ra) {
     v = (v < 0.0) ? 0.0 : (0.999 < v) ? 0.999 : v;
     ra.rgb[o3 + c] = (uint8_t)(uint32_t)(v * 256);
   }
+}
+__global__ __launch_bounds__(256) void yk_reduce_samples(ReduceArgs ra) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < ra.npix_slots; p += gridDim.x * blockDim.x)
+    reduce_slot(ra, p);
 }
 
 // ykgpu_math_div: the renderer's vector / scalar division (divs_fast) on a buffer (diagnostic).
@@ -563,11 +539,12 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
 // instance 0.6% through SGPR spills); bit 2: the yk::xor128 engine (YK_RNG_XOR128)
 template <bool kSceneInLds, int kMode>
 __global__ __launch_bounds__(kBlock)
-#ifdef YK_RENDER_VGPRS
-__attribute__((amdgpu_num_vgpr(YK_RENDER_VGPRS)))
-#endif
 #if YK_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
+#else
+// production instances at <= 128 VGPRs (one short of their natural 129): 3 x 128 of a SIMD's 512
+// leave 128, four yk_mt_warmup waves of 32 (the counting instances keep their registers)
+__attribute__((amdgpu_waves_per_eu((kMode & 1) ? 1 : 4, 8)))
 #endif
 void yk_render_persistent(KernelArgs ka) {
   constexpr bool kCount = (kMode & 1) != 0;
@@ -780,16 +757,6 @@ void yk_render_persistent(KernelArgs ka) {
 #else
         uint32_t sp = 0;
 #endif
-#if YK_WIDE && YK_SPEC_LEAF
-        int32_t pend = ykbvh::kEmptyLeaf;  // the parked leaf (kEmptyLeaf: none)
-#define YK_POP_NODE()          \
-  if (top == stk) {            \
-    node = ykbvh::kEmptyLeaf;  \
-  } else {                     \
-    top -= kBlock;             \
-    node = *top;               \
-  }
-#endif
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
@@ -842,15 +809,8 @@ void yk_render_persistent(KernelArgs ka) {
                 top = stk;
                 node = ykbvh::kEmptyLeaf;
               }
-#if !YK_SPEC_LEAF
               continue;
-#endif
             }
-#if YK_SPEC_LEAF
-            else {
-              YK_POP_NODE();
-            }
-#endif
 #else
             // near / far distances of both children per axis, one packed FMA per pair:
             // t = plane*(1/d) - o*(1/d)
@@ -883,26 +843,9 @@ void yk_render_persistent(KernelArgs ka) {
               continue;
             }
 #endif
-          }
-#if YK_WIDE && YK_SPEC_LEAF
-          // park a leaf reached while none is parked, and traverse on
-          if (node < 0 && node != ykbvh::kEmptyLeaf && pend == ykbvh::kEmptyLeaf) {
-            pend = node;
-            YK_POP_NODE();
-          }
-          // test the parked leaves together once enough lanes hold one (a finished lane counts
-          // as ready): a wave-uniform branch, skipped on the other trips (an empty parked slot
-          // is the empty leaf: no spheres)
-          const bool ready = pend != ykbvh::kEmptyLeaf || node == ykbvh::kEmptyLeaf;
-          if (__builtin_popcountll(__ballot(ready)) * 16 >= __builtin_popcountll(__ballot(1)) * YK_SPEC_LEAF) {
-            const int32_t leaf = pend;
-            pend = ykbvh::kEmptyLeaf;
-#else
-          else {
-            const int32_t leaf = node;
-#endif
+          } else {
             YK_STAMP(2);  // interior nodes since the last stamp
-            const uint32_t v = ~(uint32_t)leaf, first = v >> 4, cnt = v & 15u;
+            const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
 #ifdef YK_LEAF_UNROLL
 #pragma unroll YK_LEAF_UNROLL
 #endif
@@ -951,10 +894,7 @@ void yk_render_persistent(KernelArgs ka) {
             }
             YK_STAMP(6);  // this leaf
           }
-#if YK_WIDE && YK_SPEC_LEAF
-          if (node == ykbvh::kEmptyLeaf && pend == ykbvh::kEmptyLeaf) break;
-#undef YK_POP_NODE
-#elif YK_WIDE
+#if YK_WIDE
           if (top == stk) break;
           top -= kBlock;
           node = *top;
@@ -972,68 +912,10 @@ void yk_render_persistent(KernelArgs ka) {
           // candidate of a ray, so its refined reciprocal is computed once
           const bool a_ok = ykd::div_range(a);
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
-#if YK_CAND_COMPACT
-          // As one wave-wide list: most lanes hold one candidate, a few up to four, and per-lane
-          // blocks would run max-over-lanes times.  The owners post (sphere id, owner lane) at list
-          // positions from ballot prefix counts; every lane of the branch evaluates entries
-          // rank, rank + n, ... with the owner's ray fetched by lane shuffles; the roots come back
-          // through LDS and each owner merges its own under the closest-hit rule, which is a min
-          // with ties to the larger id (order-free).  The list lives in this wave's columns of the
-          // traversal stacks, free again now: ids in rows 0-3, roots (f64) in rows 4-11
-          // (stack_entries >= 12, upload_tree).
-          {
-            const bool e0 = nc > 0 && l0 <= ustar_f, e1 = nc > 1 && l1 <= ustar_f;
-            const bool e2 = nc > 2 && l2 <= ustar_f, e3 = nc > 3 && l3 <= ustar_f;
-            const uint64_t below = (1ull << lane) - 1ull;
-            const uint64_t m0 = __ballot(e0), m1 = __ballot(e1), m2 = __ballot(e2), m3 = __ballot(e3);
-            const uint32_t p1 = __popcll(m0), p2 = p1 + __popcll(m1), p3 = p2 + __popcll(m2);
-            const uint32_t total = p3 + __popcll(m3);
-            uint32_t* const wcol = (uint32_t*)stk - lane;  // this wave's column 0, row 0
-            const uint32_t g0 = __popcll(m0 & below), g1 = p1 + __popcll(m1 & below);
-            const uint32_t g2 = p2 + __popcll(m2 & below), g3 = p3 + __popcll(m3 & below);
-            const uint32_t tag = lane << 16;
-            if (e0) wcol[(g0 >> 6) * kBlock + (g0 & 63u)] = c0 | tag;
-            if (e1) wcol[(g1 >> 6) * kBlock + (g1 & 63u)] = c1 | tag;
-            if (e2) wcol[(g2 >> 6) * kBlock + (g2 & 63u)] = c2 | tag;
-            if (e3) wcol[(g3 >> 6) * kBlock + (g3 & 63u)] = c3 | tag;
-            auto root_at = [&](uint32_t g) -> double* {
-              return (double*)(wcol + (4u + (g >> 5)) * kBlock) + (g & 31u);
-            };
-            const uint64_t act = __ballot(1);
-            const uint32_t nact = __popcll(act), rank = __popcll(act & below);
-            for (uint32_t base = 0; base < total; base += nact) {  // wave-uniform
-              const uint32_t g = base + rank;
-              const bool mine = g < total;
-              const uint32_t w = mine ? wcol[(g >> 6) * kBlock + (g & 63u)] : lane << 16;
-              const int src = (int)(w >> 16);
-              // the owner's ray: every lane of the branch takes part in the shuffles
-              const v3 wo = {__shfl(o.x, src), __shfl(o.y, src), __shfl(o.z, src)};
-              const v3 wd = {__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src)};
-              const double wa = __shfl(a, src), wra = __shfl(ra, src);
-              if (mine) {
-                *root_at(g) = candidate_root(geo, w & 0xffffu, wo, wd, wa, wra, ykd::div_range(wa), ka.t_min, hit);
-              }
-            }
-            // closest wins; an exact tie goes to the later tuple index (hittable_list.hpp:36-43)
-            auto merge = [&](bool e, uint32_t g, uint32_t id) {
-              if (!e) return;
-              const double r = *root_at(g);
-              if (r < hit.T || (r == hit.T && (int)id > hit.hid)) {
-                hit.T = r;
-                hit.hid = (int)id;
-              }
-            };
-            merge(e0, g0, c0);
-            merge(e1, g1, c1);
-            merge(e2, g2, c2);
-            merge(e3, g3, c3);
-          }
-#else
           if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 1 && l1 <= ustar_f) exact_candidate(geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 2 && l2 <= ustar_f) exact_candidate(geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 3 && l3 <= ustar_f) exact_candidate(geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
-#endif
         }
       }
       if (linear) {
@@ -1652,6 +1534,7 @@ struct ykgpu_context {
   hipStream_t aux = nullptr;  // the MT warm-ups run here, beside the render launches
   hipStream_t red = nullptr;  // the ordered reduces run here, beside the next render launch
   hipStream_t alt = nullptr;  // odd render launches: a launch starts while the previous drains
+  hipStream_t ren = nullptr;  // even render launches (alt and ren: the device's top stream priority)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> lev;  // per launch: warm-up start, render start, reduce start, end
   uint32_t lev_used = 0;
@@ -1803,6 +1686,35 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride)
   return YK_OK;
 }
 
+// Render streams get the device's top priority (YKGPU_RENDER_PRIO=0: default priority, A/B): when
+// a launch drains, the queued warm-up and reduce blocks would otherwise take the CUs it frees
+// before the next launch's workgroups (one per CU, 768 threads and most of the LDS) fit.
+hipError_t create_render_stream(hipStream_t* s) {
+  int least = 0, greatest = 0;
+  const char* e = std::getenv("YKGPU_RENDER_PRIO");
+  if ((e && std::atoi(e) == 0) || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
+// Colour buffers in flight (YKGPU_COL_RING overrides): up to 4, within kColRingBytes
+constexpr uint64_t kColRingBytes = 24ull << 30;
+uint32_t col_ring(uint32_t nps, uint32_t K) {
+  const uint64_t one = 8ull * kColStride * nps * K;
+  uint32_t r = (uint32_t)std::max<uint64_t>(2, std::min<uint64_t>(4, kColRingBytes / std::max<uint64_t>(1, one)));
+  if (const char* e = std::getenv("YKGPU_COL_RING")) r = (uint32_t)std::max(2, std::min(8, std::atoi(e)));
+  return r;
+}
+
+// Reduce grid: grid-stride over the slots, at most 4 blocks per CU (YKGPU_RED_BLOCKS overrides;
+// 0 = one thread per slot), so a reduce never floods the CUs a render launch is about to take
+uint32_t reduce_blocks(const ykgpu_context* ctx, uint32_t nps) {
+  uint32_t cap = (uint32_t)ctx->cus * 4;
+  if (const char* e = std::getenv("YKGPU_RED_BLOCKS")) cap = (uint32_t)std::max(0, std::atoi(e));
+  const uint32_t full = (nps + 255) / 256;
+  return cap ? std::max(1u, std::min(full, cap)) : full;
+}
+
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
   const bool f32 = p->precision == YK_PRECISION_FP32;
@@ -1873,8 +1785,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (welem * nps * K)));
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
-  // two colour buffers: reduce c (stream red) overlaps render c + 1
-  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)2 * nps * K * kColStride, sizeof(double)))) return rc;
+  // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
+  // reduce c (stream red) overlaps the renders after it
+  const uint32_t kColRing = col_ring(nps, K);
+  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)kColRing * nps * K * kColStride, sizeof(double)))) return rc;
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
@@ -1976,6 +1890,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ctx->lev_used = 6 * nlaunch;
   YK_HIP(hipStreamWaitEvent(ctx->red, ctx->ev0, 0));
   YK_HIP(hipStreamWaitEvent(ctx->alt, ctx->ev0, 0));
+  YK_HIP(hipStreamWaitEvent(ctx->ren, ctx->ev0, 0));
   auto warm = [&](uint32_t c) -> int {
     hipEvent_t* ev = &ctx->lev[6 * c];
     if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
@@ -1986,9 +1901,11 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
       if (f32)
-        hipLaunchKernelGGL(yk_mt_warmup<false>, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+        hipLaunchKernelGGL((yk_mt_warmup<false, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      else if (wa.lens)
+        hipLaunchKernelGGL((yk_mt_warmup<true, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else
-        hipLaunchKernelGGL(yk_mt_warmup<true>, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+        hipLaunchKernelGGL((yk_mt_warmup<true, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       YK_HIP(hipGetLastError());
     }
     YK_HIP(hipEventRecord(ev[1], ctx->aux));
@@ -2001,7 +1918,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     hipEvent_t* ev = &ctx->lev[6 * c];
     const uint32_t s0 = sched[c].first, ks = sched[c].second;
     const uint32_t nsl = nps * ks;
-    double* col = ctx->d_col + (size_t)(c % 2) * nps * K * kColStride;
+    double* col = ctx->d_col + (size_t)(c % kColRing) * nps * K * kColStride;
     ka.s0 = s0;
     ka.nsl = nsl;
     ka.col = col;
@@ -2011,12 +1928,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
     // only on its own x_397 and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
-    const hipStream_t rs = (c & 1) ? ctx->alt : st;
+    const hipStream_t rs = (c & 1) ? ctx->alt : ctx->ren;
     const size_t lanes = (size_t)grid * kBlock;
     ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (c & 1) * lanes * ykd::kMtN : nullptr;
     ka.id_scratch = ctx->d_ids + (c & 1) * lanes * ctx->id_stride;
     YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its x_397
-    if (c >= 2) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - 2) + 5], 0));  // its colour buffer
+    if (c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
     ka.pixel_counter = ctx->d_counter + c;
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
@@ -2036,7 +1953,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ra.last = s0 + ks == spp;
     YK_HIP(hipStreamWaitEvent(ctx->red, ev[3], 0));
     YK_HIP(hipEventRecord(ev[4], ctx->red));
-    hipLaunchKernelGGL(yk_reduce_samples, dim3((nps + 255) / 256), dim3(256), 0, ctx->red, ra);
+    hipLaunchKernelGGL(yk_reduce_samples, dim3(reduce_blocks(ctx, nps)), dim3(256), 0, ctx->red, ra);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[5], ctx->red));
     if (c + kWarmRing < nlaunch && (rc = warm(c + kWarmRing))) return rc;
@@ -2083,6 +2000,15 @@ int finish_stats(ykgpu_context* ctx) {
     busy += b - std::min<double>(b, std::max<double>(0.0, ov));
   }
   ctx->stats.render_busy_ms = busy;
+  if (std::getenv("YKGPU_TIMELINE")) {  // diagnostic: per-launch event times (ms from the call's start)
+    for (uint32_t k = 0; k + 5 < ctx->lev_used; k += 6) {
+      float t[6];
+      for (int q = 0; q < 6; ++q) YK_HIP(hipEventElapsedTime(&t[q], ctx->ev0, ctx->lev[k + q]));
+      std::fprintf(stderr, "launch %u: warm %8.3f %8.3f  render %8.3f %8.3f  reduce %8.3f %8.3f\n", k / 6, t[0], t[1],
+                   t[2], t[3], t[4], t[5]);
+    }
+    std::fprintf(stderr, "call %8.3f\n", ms);
+  }
   ctx->stats.warmup_ms = tw;
   ctx->stats.kernel_ms = tr;
   ctx->stats.resolve_ms = tp;
@@ -2214,7 +2140,7 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->alt, hipStreamNonBlocking) != hipSuccess ||
+      create_render_stream(&ctx->alt) != hipSuccess || create_render_stream(&ctx->ren) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
     ykgpu_context_destroy(ctx);
@@ -2250,6 +2176,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->red) (void)hipStreamDestroy(ctx->red);
   if (ctx->alt) (void)hipStreamDestroy(ctx->alt);
+  if (ctx->ren) (void)hipStreamDestroy(ctx->ren);
   delete ctx;
   return YK_OK;
 }
