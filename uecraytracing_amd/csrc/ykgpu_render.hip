@@ -6,7 +6,7 @@
 //
 // Execution model:
 //   * a render call is a sequence of LAUNCHES of K samples per pixel (8, 32, then at most
-//     kLaunchSpp = 64; 1920x1080x512: 8, 32, 7 x 64, 24).  Per launch: yk_mt_warmup (second
+//     kLaunchSpp = 32; 1920x1080x512: 8, 15 x 32, 24).  Per launch: yk_mt_warmup (second
 //     stream: every sample's mt19937 seeding walk and, for the FP64 kernel, its start draws —
 //     jitter and lens — as a StartRec), yk_render_persistent (the paths), yk_reduce_samples (the
 //     reference's strictly sequential per-pixel sum and to_color3b, third stream).
@@ -1628,9 +1628,10 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, int grid, bool need_m
 constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colours per launch at most
 // samples per pixel per launch at most: many mid-sized launches beat a few big ones, because the
 // launches alternate between two streams and each one's drain overlaps the next one's start
-// (1920x1080x512 259.5 -> 254.0 ms at 64 spp/launch, its 8-way tile 35.1 -> 34.2 ms)
+// (round 1, 1920x1080x512 259.5 -> 254.0 ms at 64 spp/launch; with the render
+// streams at top priority, bench 205.5 ms at 64, 199.6 at 32, 199.8 at 24, 206.3 at 16)
 #ifndef YK_LAUNCH_SPP
-#define YK_LAUNCH_SPP 64
+#define YK_LAUNCH_SPP 32
 #endif
 constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
 // x_397 buffers: the warm-ups run on ctx->aux, beside the render launches (their wave slots and
@@ -1737,13 +1738,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   rc = ensure_order(ctx, p->image_width, p->row_count,
                     p->row_count > 1 && p->row_band_log2 < 3 ? p->row_stride : 1);
   if (rc) return rc;
-  // Launch schedule (samples per pixel per launch): 8, 32, then kLaunchSpp (64) per launch, also
-  // capped by the colour budget (24 B per sample slot, kColourBytes per launch); the last launch
-  // takes a small remainder with it (1920x1080x512: 8, 32, 7 x 64, 24 = ten launches).  The first
+  // Launch schedule (samples per pixel per launch): 8, then kLaunchSpp (32) per launch, also
+  // capped by the colour budget (32 B per sample slot, kColourBytes per launch); the last launch
+  // takes a small remainder with it (1920x1080x512: 8, 15 x 32, 24 = 17 launches).  The first
   // render waits only for an 8-sample warm-up; every later warm-up is ~0.15x the render before it,
   // so it finishes underneath.  Each launch ends with the tail of its longest paths (~1 ms), but
-  // launches alternate between two streams, so that drain overlaps the next launch: ten mid-sized
-  // launches beat five large ones.  Independent of the image size, which matters
+  // launches alternate between two streams, so that drain overlaps the next launch: many
+  // mid-sized launches beat a few large ones.  Independent of the image size, which matters
   // for the per-rank tiles of N GPUs.
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
   const uint32_t spp = p->samples_per_pixel;
