@@ -90,6 +90,18 @@ static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 #define YK_WAVES_PER_EU 0
 #endif
 constexpr int kBlock = YK_BLOCK;
+// The xor128 instances draw no seed walks, so nothing needs the fourth wave slot of a SIMD: they
+// run 1024-thread workgroups (4 render waves per SIMD; the node loop is bound by LDS latency, so
+// the fourth wave pays)
+#ifndef YK_BLOCK_X128
+#define YK_BLOCK_X128 1024
+#endif
+constexpr int kBlockX128 = YK_BLOCK_X128;
+template <int kMode>
+constexpr int mode_block() {
+  return (kMode & 4) ? kBlockX128 : kBlock;
+}
+constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #ifndef YK_RENDER_PRIO
 #define YK_RENDER_PRIO 1
 #endif
@@ -538,7 +550,7 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
 // the hash's 64-bit arithmetic and two more kernel arguments cost the counter-seeded production
 // instance 0.6% through SGPR spills); bit 2: the yk::xor128 engine (YK_RNG_XOR128)
 template <bool kSceneInLds, int kMode>
-__global__ __launch_bounds__(kBlock)
+__global__ __launch_bounds__(mode_block<kMode>())
 #if YK_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
 #else
@@ -547,6 +559,7 @@ __attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
 __attribute__((amdgpu_waves_per_eu((kMode & 1) ? 1 : 4, 8)))
 #endif
 void yk_render_persistent(KernelArgs ka) {
+  constexpr int kBlk = mode_block<kMode>();
   constexpr bool kCount = (kMode & 1) != 0;
   constexpr bool kRandomSeed = (kMode & 2) != 0;
   using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
@@ -568,7 +581,7 @@ void yk_render_persistent(KernelArgs ka) {
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       uint4* dst = (uint4*)(smem + off[k]);
-      for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlock) dst[i] = src[k][i];
+      for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlk) dst[i] = src[k][i];
     }
     __syncthreads();
     nodes = smem;
@@ -577,7 +590,7 @@ void yk_render_persistent(KernelArgs ka) {
     geo = (const SphereGeo*)(smem + ka.lds_tgeo_off);
     mat = (const SphereMat*)(smem + ka.lds_mat_off);
   }
-  int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlock]
+  int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlk]
   // YK_FLAG_ONE_LANE (counting instance only): lanes 1..63 leave here, after the block's last
   // barrier, so every wave-instruction below is one lane's (the profiler's per-wave FP64 counters
   // then count that lane's executed operations exactly: DESIGN.md §5)
@@ -752,8 +765,8 @@ void yk_render_persistent(KernelArgs ka) {
         uint32_t overflow = 0;
         int32_t node = ka.bvh_root;
 #if YK_WIDE
-        int32_t* top = stk;  // this lane's traversal stack top (entries kBlock words apart)
-        const int32_t* const stk_cap = stk + ka.stack_cap * kBlock;
+        int32_t* top = stk;  // this lane's traversal stack top (entries kBlk words apart)
+        const int32_t* const stk_cap = stk + ka.stack_cap * kBlk;
 #else
         uint32_t sp = 0;
 #endif
@@ -799,11 +812,11 @@ void yk_render_persistent(KernelArgs ka) {
               // visits).  Each write lands at the current top, which moves only for a push.
               node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : ch.x));
               *top = ch.x;
-              top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlock : 0;
+              top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlk : 0;
               *top = ch.y;
-              top += (hk[1] && (hk[2] || hk[3])) ? kBlock : 0;
+              top += (hk[1] && (hk[2] || hk[3])) ? kBlk : 0;
               *top = ch.z;
-              top += (hk[2] && hk[3]) ? kBlock : 0;
+              top += (hk[2] && hk[3]) ? kBlk : 0;
               if (top > stk_cap) {  // stack full: abandon, the exact linear scan decides
                 overflow = true;
                 top = stk;
@@ -833,7 +846,7 @@ void yk_render_persistent(KernelArgs ka) {
             const bool h0 = hk[0], h1 = hk[1];
             if (h0 && h1) {
               const bool first0 = tn[0] <= tn[1];
-              stk[sp * kBlock] = first0 ? ch.y : ch.x;
+              stk[sp * kBlk] = first0 ? ch.y : ch.x;
               ++sp;
               node = first0 ? ch.x : ch.y;
               continue;
@@ -896,12 +909,12 @@ void yk_render_persistent(KernelArgs ka) {
           }
 #if YK_WIDE
           if (top == stk) break;
-          top -= kBlock;
+          top -= kBlk;
           node = *top;
 #else
           if (sp == 0) break;
           --sp;
-          node = stk[sp * kBlock];
+          node = stk[sp * kBlk];
 #endif
         }
         YK_STAMP(2);
@@ -1172,7 +1185,8 @@ __device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, 
 // workgroup, as in the FP64 kernel.  kMode bit 0: the work counters; bit 2: the yk::xor128
 // engine (as for the FP64 kernel)
 template <bool kSceneInLds, int kMode>
-__global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
+__global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs ka) {
+  constexpr int kBlk = mode_block<kMode>();
   constexpr bool kCount = (kMode & 1) != 0;
   using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1189,14 +1203,14 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       uint4* dst = (uint4*)(smem + off[k]);
-      for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlock) dst[i] = src[k][i];
+      for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlk) dst[i] = src[k][i];
     }
     __syncthreads();
     nodes = smem;
     leaf_geo = (const float4*)(smem + ka.lds_geo_off);
     leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
   }
-  int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlock]
+  int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlk]
 #if YK_RENDER_PRIO
   __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);  // over the co-resident warm-up waves, as in FP64
 #endif
@@ -1281,7 +1295,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
         uint32_t overflow = 0;  // a VGPR, not a lane-mask bool (see the FP64 kernel)
         int32_t node = ka.bvh_root;
         int32_t* top = stk;
-        const int32_t* const stk_cap = stk + ka.stack_cap * kBlock;
+        const int32_t* const stk_cap = stk + ka.stack_cap * kBlk;
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
@@ -1307,11 +1321,11 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
             if (hk[0] || hk[1] || hk[2] || hk[3]) {
               node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : ch.x));
               *top = ch.x;
-              top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlock : 0;
+              top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlk : 0;
               *top = ch.y;
-              top += (hk[1] && (hk[2] || hk[3])) ? kBlock : 0;
+              top += (hk[1] && (hk[2] || hk[3])) ? kBlk : 0;
               *top = ch.z;
-              top += (hk[2] && hk[3]) ? kBlock : 0;
+              top += (hk[2] && hk[3]) ? kBlk : 0;
               if (top > stk_cap) {  // stack full: abandon, the linear scan decides
                 overflow = 1;
                 top = stk;
@@ -1337,7 +1351,7 @@ __global__ __launch_bounds__(kBlock) void yk_render_f32(KernelArgs ka) {
             }
           }
           if (top == stk) break;
-          top -= kBlock;
+          top -= kBlk;
           node = *top;
         }
         if (overflow != 0) linear = true;
@@ -1504,10 +1518,14 @@ struct DevTree {
   int32_t root = 0;              // root code (byte offset of the root node, or a leaf code)
   uint32_t depth = 0, n_nodes = 0;
   double origin_bound = 0;  // |o|_inf beyond which a ray takes the linear scan (< 0: every ray)
-  bool in_lds = false;
-  uint32_t lds_bytes = 0, geo_off = 0, ids_off = 0, stack_off = 0, stack_cap = 0, stack_entries = 0;
-  uint32_t tgeo_off = 0, mat_off = 0;  // shading tables in LDS (FP64 kernel), 0: none
-  int grid = 0;  // persistent blocks: occupancy x CUs
+  uint32_t geo_off = 0, ids_off = 0;  // leaf geometry and ids in LDS, after the nodes
+  // LDS plan per workgroup size: [0] kBlock (mt19937 instances), [1] kBlockX128 (xor128)
+  struct Plan {
+    bool in_lds = false;
+    uint32_t lds_bytes = 0, stack_off = 0, stack_cap = 0, stack_entries = 0;
+    uint32_t tgeo_off = 0, mat_off = 0;  // shading tables in LDS (FP64 kernel), 0: none
+    int grid = 0;                        // persistent blocks: occupancy x CUs
+  } plan[2];
   void release() {
     (void)hipFree(nodes);
     (void)hipFree(leaf_geo);
@@ -1598,8 +1616,7 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
   return YK_OK;
 }
 
-int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, int grid, bool need_mt) {
-  const size_t lanes = (size_t)grid * kBlock;
+int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, size_t lanes, bool need_mt) {
   // mt19937 fallback engines: 624 words per persistent lane (not needed by xor128)
   if (need_mt && (lanes > ctx->scratch_lanes || !ctx->d_mt)) {
     (void)hipFree(ctx->d_mt);
@@ -1721,8 +1738,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const bool f32 = p->precision == YK_PRECISION_FP32;
   const bool x128 = p->rng == YK_RNG_XOR128;  // no x_397 warm-ups, no MT scratch
   const DevTree& tree = f32 ? ctx->t32 : ctx->t64;
-  const int grid = tree.grid;
-  int rc = ensure_scratch(ctx, p->max_depth, grid, !x128);
+  const DevTree::Plan& plan = tree.plan[x128 ? 1 : 0];
+  const int grid = plan.grid, block = block_of(x128);
+  int rc = ensure_scratch(ctx, p->max_depth, (size_t)grid * block, !x128);
   if (rc) return rc;
   // YK_SEED_RANDOM_DEVICE without a key: one from std::random_device per call (source.cpp:159)
   uint64_t seed_key = 0;
@@ -1752,7 +1770,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // A launch of few pixels still gets enough slots to fill the persistent grid (16 per lane):
   // a thin row tile at high spp would otherwise run dozens of launches that each pay a ramp and
   // a drain.  Neither floor nor cap exceeds the colour budget or 2^31 slots.
-  const uint64_t fill_spp = ((uint64_t)grid * kBlock * 16 + nps - 1) / nps;
+  const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>({spp, kColourBytes / (8ull * kColStride * nps), std::max<uint64_t>(kLaunchSpp, fill_spp),
                              ((1ull << 31) - 1) / nps}));
@@ -1816,10 +1834,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.n_nodes = tree.n_nodes;
   ka.lds_geo_off = tree.geo_off;
   ka.lds_ids_off = tree.ids_off;
-  ka.lds_tgeo_off = tree.tgeo_off;
-  ka.lds_mat_off = tree.mat_off;
-  ka.lds_stack_off = tree.stack_off;
-  ka.stack_cap = tree.stack_cap;
+  ka.lds_tgeo_off = plan.tgeo_off;
+  ka.lds_mat_off = plan.mat_off;
+  ka.lds_stack_off = plan.stack_off;
+  ka.stack_cap = plan.stack_cap;
   ka.nodes = tree.nodes;
   ka.leaf_geo = (const SphereGeo*)tree.leaf_geo;  // float4 records for the FP32 kernel
   ka.leaf_ids = tree.leaf_ids;
@@ -1930,7 +1948,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     // only on its own x_397 and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
     const hipStream_t rs = (c & 1) ? ctx->alt : ctx->ren;
-    const size_t lanes = (size_t)grid * kBlock;
+    const size_t lanes = (size_t)grid * block;
     ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (c & 1) * lanes * ykd::kMtN : nullptr;
     ka.id_scratch = ctx->d_ids + (c & 1) * lanes * ctx->id_stride;
     YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its x_397
@@ -1939,12 +1957,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (f32)
-      hipLaunchKernelGGL(f32_kernel(tree.in_lds, (count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(kBlock),
-                         tree.lds_bytes, rs, ka);
+      hipLaunchKernelGGL(f32_kernel(plan.in_lds, (count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(block),
+                         plan.lds_bytes, rs, ka);
     else
-      hipLaunchKernelGGL(fp64_kernel(tree.in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
+      hipLaunchKernelGGL(fp64_kernel(plan.in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
                                                       (x128 ? 4 : 0)),
-                         dim3(grid), dim3(kBlock), tree.lds_bytes, rs, ka);
+                         dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[3], rs));
     ra.col = col;
@@ -2022,11 +2040,12 @@ int finish_stats(ykgpu_context* ctx) {
 }
 
 // Builds one BVH over the scene and uploads it into t: `geo` holds the tuple-order geometry the
-// kernel's leaves read (`elem` bytes per sphere), stored in leaf order; kern_lds / kern_glob are
-// the kernel instances that read the tree from LDS / global memory (for the occupancy).
+// kernel's leaves read (`elem` bytes per sphere), stored in leaf order; kern[v][lds] are the kernel
+// instances of workgroup size v (kBlock, kBlockX128) that read the tree from global memory / LDS
+// (for the occupancy).
 int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
                 double cam_ext, const ykbvh::Options& opt, const void* geo, size_t elem, size_t table_bytes,
-                RenderKernel kern_lds, RenderKernel kern_glob) {
+                const RenderKernel (&kern)[2][2]) {
   const uint32_t count = (uint32_t)radii.size();
   const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
   if (bvh.depth > ykbvh::kMaxDepth) return fail(YK_ERR_INVALID, "BVH deeper than the traversal stack");
@@ -2056,44 +2075,49 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   t.n_nodes = (uint32_t)snodes.size();
   // LDS layout: [nodes][leaf geometry][leaf ids][tuple-order geometry][materials][traversal
   // stacks].  The tables (table_bytes per sphere: the FP64 kernel's candidate and shading reads,
-  // 0 for the FP32 kernel) go wherever the tree goes: the LDS instance reads both from LDS
+  // 0 for the FP32 kernel) go wherever the tree goes: the LDS instance reads both from LDS.  One
+  // plan per workgroup size (the stacks are per lane).
   auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t scene_bytes = a16(t.n_nodes * sizeof(DevNode)) + a16(count * elem) + a16(count * sizeof(uint32_t));
   const size_t tgeo_bytes = table_bytes ? a16(count * sizeof(SphereGeo)) : 0;
   const size_t mat_bytes = table_bytes ? a16(count * sizeof(SphereMat)) : 0;
-  // a CU holds one workgroup of >= 768 threads (768 / kBlock of smaller ones); 2 KB below the
-  // share: the hardware's allocation granularity (3 blocks of 54144 bytes measured only 2
-  // resident per CU)
-  const size_t budget = (size_t)160 * 1024 / (kBlock >= 768 ? 1 : 768 / kBlock) - 2048;
-  const size_t min_stacks = (size_t)12 * kBlock * 4;
-  t.in_lds = scene_bytes + tgeo_bytes + mat_bytes + min_stacks <= budget;
-  const size_t tables = t.in_lds ? tgeo_bytes + mat_bytes : 0;
-#if YK_WIDE
-  // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries); the
-  // capacity is what still fits the budget (at least 8); a lane that would exceed it abandons the
-  // traversal for the exact linear scan.  Pushes write unconditionally at the current top (up to
-  // 3 past the capacity): +4 entries.
-  {
-    const size_t used = t.in_lds ? scene_bytes + tables : 0;
-    const uint32_t fit = used + min_stacks <= budget ? (uint32_t)((budget - used) / (kBlock * 4)) : 12u;
-    t.stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
-    t.stack_entries = t.stack_cap + 4;
-  }
-#else
-  t.stack_cap = bvh.depth + 1;
-  t.stack_entries = bvh.depth + 1;
-#endif
   t.geo_off = (uint32_t)a16(t.n_nodes * sizeof(DevNode));
   t.ids_off = t.geo_off + (uint32_t)a16(count * elem);
-  t.tgeo_off = t.in_lds && table_bytes ? (uint32_t)scene_bytes : 0u;
-  t.mat_off = t.in_lds && table_bytes ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
-  t.stack_off = t.in_lds ? (uint32_t)(scene_bytes + tables) : 0u;
-  t.lds_bytes = t.stack_off + t.stack_entries * kBlock * (uint32_t)sizeof(int32_t);
-  int per_cu = 0;
-  const hipError_t e =
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, t.in_lds ? kern_lds : kern_glob, kBlock, t.lds_bytes);
-  if (e != hipSuccess || per_cu < 1) per_cu = 1;
-  t.grid = per_cu * ctx->cus;
+  for (int v = 0; v < 2; ++v) {
+    DevTree::Plan& pl = t.plan[v];
+    const int blk = block_of(v == 1);
+    // a CU holds one workgroup of >= 768 threads (768 / blk of smaller ones); 2 KB below the
+    // share: the hardware's allocation granularity (3 blocks of 54144 bytes measured only 2
+    // resident per CU)
+    const size_t budget = (size_t)160 * 1024 / (blk >= 768 ? 1 : 768 / blk) - 2048;
+    const size_t min_stacks = (size_t)12 * blk * 4;
+    pl.in_lds = scene_bytes + tgeo_bytes + mat_bytes + min_stacks <= budget;
+    const size_t tables = pl.in_lds ? tgeo_bytes + mat_bytes : 0;
+#if YK_WIDE
+    // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries);
+    // the capacity is what still fits the budget (at least 8); a lane that would exceed it
+    // abandons the traversal for the exact linear scan.  Pushes write unconditionally at the
+    // current top (up to 3 past the capacity): +4 entries.
+    {
+      const size_t used = pl.in_lds ? scene_bytes + tables : 0;
+      const uint32_t fit = used + min_stacks <= budget ? (uint32_t)((budget - used) / (blk * 4)) : 12u;
+      pl.stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
+      pl.stack_entries = pl.stack_cap + 4;
+    }
+#else
+    pl.stack_cap = bvh.depth + 1;
+    pl.stack_entries = bvh.depth + 1;
+#endif
+    pl.tgeo_off = pl.in_lds && table_bytes ? (uint32_t)scene_bytes : 0u;
+    pl.mat_off = pl.in_lds && table_bytes ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
+    pl.stack_off = pl.in_lds ? (uint32_t)(scene_bytes + tables) : 0u;
+    pl.lds_bytes = pl.stack_off + pl.stack_entries * blk * (uint32_t)sizeof(int32_t);
+    int per_cu = 0;
+    const RenderKernel k = kern[v][pl.in_lds ? 1 : 0];
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, blk, pl.lds_bytes);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    pl.grid = per_cu * ctx->cus;
+  }
   return YK_OK;
 }
 
@@ -2234,15 +2258,18 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   };
   ykbvh::Options bopt;
   bopt.max_leaf = leaf_env("YKGPU_BVH_LEAF", 1);
+  const RenderKernel k64[2][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
+                                  {fp64_kernel(false, 4), fp64_kernel(true, 4)}};
   int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, geo.data(), sizeof(SphereGeo),
-                       sizeof(SphereGeo) + sizeof(SphereMat), fp64_kernel(true, 0), fp64_kernel(false, 0));
+                       sizeof(SphereGeo) + sizeof(SphereMat), k64);
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
   fopt.max_leaf = leaf_env("YKGPU_BVH_LEAF_F32", 2);
   fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
   fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
-  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4), 0,
-                   f32_kernel(true, 0), f32_kernel(false, 0));
+  const RenderKernel k32[2][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
+                                  {f32_kernel(false, 4), f32_kernel(true, 4)}};
+  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4), 0, k32);
   if (rc) return rc;
   // the float bound assumes neither underflow nor overflow: a scene outside that
   // scale renders FP32 with the linear scan throughout
