@@ -1651,6 +1651,14 @@ constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colou
 #define YK_LAUNCH_SPP 32
 #endif
 constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
+// ... and at least kLaunchSlots sample slots per launch when the tile is small: a launch has a
+// fixed cost (its warm-up, the ramp of its persistent grid, a reduce), so a thin row tile needs
+// more samples per launch (8-way tile of 1920x1080x512, 135 rows: 31.5 ms at 32 spp per launch,
+// 28.8 at 64, 28.2 at 128, 29.4 at 256 — the full frame's best launch, 32 spp, is 66M slots)
+#ifndef YK_LAUNCH_SLOTS
+#define YK_LAUNCH_SLOTS (1u << 25)
+#endif
+constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
 // x_397 buffers: the warm-ups run on ctx->aux, beside the render launches (their wave slots and
 // VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots idle), into
 // a ring of min(launches, kWarmBytes / slot) slots, at least 3; warm-up c waits for the render of
@@ -1771,9 +1779,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // a thin row tile at high spp would otherwise run dozens of launches that each pay a ramp and
   // a drain.  Neither floor nor cap exceeds the colour budget or 2^31 slots.
   const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
+  const uint64_t slot_spp = (kLaunchSlots + nps - 1) / nps;
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>({spp, kColourBytes / (8ull * kColStride * nps), std::max<uint64_t>(kLaunchSpp, fill_spp),
-                             ((1ull << 31) - 1) / nps}));
+      1, std::min<uint64_t>({spp, kColourBytes / (8ull * kColStride * nps),
+                             std::max<uint64_t>({kLaunchSpp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
   for (uint32_t s0 = 0, k = std::min(kFirstLaunch, kmax); s0 < spp;) {
     uint32_t take = std::min(k, spp - s0);
