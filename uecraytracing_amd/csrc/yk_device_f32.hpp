@@ -36,9 +36,17 @@ __device__ __forceinline__ v3 of(const double* p) { return {(float)p[0], (float)
 // fixed point that does not depend on the start: for every positive float s in [2^-100, 2^100]
 // the loop started at the correctly rounded sqrtf(s) ends at the reference's value (checked
 // exhaustively over all 2^31 positive floats by tools/fsqrt_check.c: every float terminates,
-// at most 80 reference iterations, and only one input — outside that range — differs).
+// at most 80 reference iterations, and only one input — outside that range — differs).  One
+// step from sqrtf(s) already lands on that fixed point (the argument of DESIGN.md §3 holds for any
+// binary format; tools/fsqrt_check.c confirms it for every float in [2^-100, 2^100]), so inside
+// the range the device returns it without the confirming second division.
 __device__ __forceinline__ float nsqrt(float s, uint32_t& iters) {
-  float x = (s >= 0x1p-100f && s <= 0x1p100f) ? __builtin_sqrtf(s) : s * 0.5f;
+  if (s >= 0x1p-100f && s <= 0x1p100f) {
+    const float r = __builtin_sqrtf(s);
+    ++iters;
+    return (r + s / r) * 0.5f;
+  }
+  float x = s * 0.5f;
   float prev = 0.0f;
   for (int guard = 0; x != prev && guard < 4096; ++guard) {  // the bound only matters for NaN/inf
     prev = x;

@@ -1195,13 +1195,17 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
   const char* __restrict__ nodes = (const char*)ka.nodes;
   const float4* __restrict__ leaf_geo = (const float4*)ka.leaf_geo;
   const uint32_t* __restrict__ leaf_ids = ka.leaf_ids;
+  const float4* __restrict__ geo_f = ka.geo_f;  // tuple order: hit records
+  const SphereMat* __restrict__ mat = ka.mat;   // shading, attenuation unwind
   if (kSceneInLds) {
-    const uint4* src[3] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids};
-    const uint32_t off[3] = {0u, ka.lds_geo_off, ka.lds_ids_off};
-    const uint32_t n16[3] = {(ka.n_nodes * (uint32_t)sizeof(DevNode) + 15u) / 16u, ka.nspheres,
-                             (ka.nspheres + 3u) / 4u};
+    // as in the FP64 kernel: the BVH, its leaf geometry and ids, and the tuple-order tables
+    const uint4* src[5] = {(const uint4*)ka.nodes, (const uint4*)ka.leaf_geo, (const uint4*)ka.leaf_ids,
+                           (const uint4*)ka.geo_f, (const uint4*)ka.mat};
+    const uint32_t off[5] = {0u, ka.lds_geo_off, ka.lds_ids_off, ka.lds_tgeo_off, ka.lds_mat_off};
+    const uint32_t n16[5] = {(ka.n_nodes * (uint32_t)sizeof(DevNode) + 15u) / 16u, ka.nspheres,
+                             (ka.nspheres + 3u) / 4u, ka.nspheres, ka.nspheres * 4u};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 5; ++k) {
       uint4* dst = (uint4*)(smem + off[k]);
       for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlk) dst[i] = src[k][i];
     }
@@ -1209,6 +1213,8 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
     nodes = smem;
     leaf_geo = (const float4*)(smem + ka.lds_geo_off);
     leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
+    geo_f = (const float4*)(smem + ka.lds_tgeo_off);
+    mat = (const SphereMat*)(smem + ka.lds_mat_off);
   }
   int32_t* const stk = (int32_t*)(smem + ka.lds_stack_off) + threadIdx.x;  // [sp * kBlk]
 #if YK_RENDER_PRIO
@@ -1391,8 +1397,8 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
       bool front = false;
       ykf::v3 vn = d;
       if (hid >= 0) {
-        const float4 sg = ka.geo_f[hid];
-        m = ka.mat[hid];
+        const float4 sg = geo_f[hid];
+        m = mat[hid];
         p = ykf::add(o, ykf::mul(d, T));  // ray::at
         const ykf::v3 outward = ykf::divs(ykf::sub(p, ykf::v3{sg.x, sg.y, sg.z}), (float)m.radius);
         front = ykf::dot(d, outward) < 0;
@@ -1466,7 +1472,7 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
         st2 = (st2 >> 16) | (st3 << 16);
         st3 = (st3 >> 16) | (nstk > kStackRegs ? ((uint32_t)id_spill[nstk - kStackRegs - 1] << 16) : 0u);
         --nstk;
-        const SphereMat m = ka.mat[id];
+        const SphereMat m = mat[id];
         L_r = m.ar * L_r;
         L_g = m.ag * L_g;
         L_b = m.ab * L_b;
@@ -2053,7 +2059,7 @@ int finish_stats(ykgpu_context* ctx) {
 // instances of workgroup size v (kBlock, kBlockX128) that read the tree from global memory / LDS
 // (for the occupancy).
 int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
-                double cam_ext, const ykbvh::Options& opt, const void* geo, size_t elem, size_t table_bytes,
+                double cam_ext, const ykbvh::Options& opt, const void* geo, size_t elem, size_t tgeo_elem,
                 const RenderKernel (&kern)[2][2]) {
   const uint32_t count = (uint32_t)radii.size();
   const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
@@ -2083,13 +2089,14 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   t.origin_bound = bvh.origin_bound;
   t.n_nodes = (uint32_t)snodes.size();
   // LDS layout: [nodes][leaf geometry][leaf ids][tuple-order geometry][materials][traversal
-  // stacks].  The tables (table_bytes per sphere: the FP64 kernel's candidate and shading reads,
-  // 0 for the FP32 kernel) go wherever the tree goes: the LDS instance reads both from LDS.  One
+  // stacks].  The tables (tgeo_elem bytes of tuple-order geometry per sphere — the FP64 kernel's
+  // SphereGeo, the FP32 kernel's float4 — and the SphereMat: candidate roots, shading, unwind) go
+  // wherever the tree goes: the LDS instance reads both from LDS.  One
   // plan per workgroup size (the stacks are per lane).
   auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
   const size_t scene_bytes = a16(t.n_nodes * sizeof(DevNode)) + a16(count * elem) + a16(count * sizeof(uint32_t));
-  const size_t tgeo_bytes = table_bytes ? a16(count * sizeof(SphereGeo)) : 0;
-  const size_t mat_bytes = table_bytes ? a16(count * sizeof(SphereMat)) : 0;
+  const size_t tgeo_bytes = tgeo_elem ? a16(count * tgeo_elem) : 0;
+  const size_t mat_bytes = tgeo_elem ? a16(count * sizeof(SphereMat)) : 0;
   t.geo_off = (uint32_t)a16(t.n_nodes * sizeof(DevNode));
   t.ids_off = t.geo_off + (uint32_t)a16(count * elem);
   for (int v = 0; v < 2; ++v) {
@@ -2117,8 +2124,8 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
     pl.stack_cap = bvh.depth + 1;
     pl.stack_entries = bvh.depth + 1;
 #endif
-    pl.tgeo_off = pl.in_lds && table_bytes ? (uint32_t)scene_bytes : 0u;
-    pl.mat_off = pl.in_lds && table_bytes ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
+    pl.tgeo_off = pl.in_lds && tgeo_elem ? (uint32_t)scene_bytes : 0u;
+    pl.mat_off = pl.in_lds && tgeo_elem ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
     pl.stack_off = pl.in_lds ? (uint32_t)(scene_bytes + tables) : 0u;
     pl.lds_bytes = pl.stack_off + pl.stack_entries * blk * (uint32_t)sizeof(int32_t);
     int per_cu = 0;
@@ -2270,7 +2277,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   const RenderKernel k64[2][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
                                   {fp64_kernel(false, 4), fp64_kernel(true, 4)}};
   int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, geo.data(), sizeof(SphereGeo),
-                       sizeof(SphereGeo) + sizeof(SphereMat), k64);
+                       sizeof(SphereGeo), k64);
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
   fopt.max_leaf = leaf_env("YKGPU_BVH_LEAF_F32", 2);
@@ -2278,7 +2285,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
   const RenderKernel k32[2][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
                                   {f32_kernel(false, 4), f32_kernel(true, 4)}};
-  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4), 0, k32);
+  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4), sizeof(float4), k32);
   if (rc) return rc;
   // the float bound assumes neither underflow nor overflow: a scene outside that
   // scale renders FP32 with the linear scan throughout
