@@ -67,16 +67,18 @@ __device__ __forceinline__ bool near_zero(v3 a) {
 
 // generate_canonical<float, 24> (random.hpp:161-183): m = max(1, (24 + 32) / 33) = 1 draw;
 // sum = float(u) (rounded to nearest), ret = sum / 2^32 (exact scaling), clamped to 1 - eps/2.
-template <class G>
+// (kLazy: the caller has checked ykd::rng_lazy_ok for the words it draws)
+template <bool kLazy = false, class G>
 __device__ __forceinline__ float canonical(G& g) {
-  const float sum = (float)ykd::rng_next(g);
+  const float sum = (float)ykd::rng_next<kLazy>(g);
   float r = sum * 0x1p-32f;
   if (r >= 1.0f) r = 1.0f - 0x1p-24f;
   return r;
 }
 // uniform_real_distribution<float>::operator() (random.hpp:273-278): c*(b-a)+a in float
+__device__ __forceinline__ float uniform_of(float c, float a, float b) { return (c * (b - a)) + a; }
 template <class G>
-__device__ __forceinline__ float uniform(G& g, float a, float b) { return (ykf::canonical(g) * (b - a)) + a; }
+__device__ __forceinline__ float uniform(G& g, float a, float b) { return uniform_of(ykf::canonical(g), a, b); }
 // vec3<float>::random(gen, -1, 1) (vec3.hpp:134-142): x, then y, then z
 template <class G>
 __device__ __forceinline__ v3 random_vec(G& g, float lo, float hi) {

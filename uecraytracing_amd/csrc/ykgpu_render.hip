@@ -1388,14 +1388,18 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
       }
     }
 
-    // ---- shade (raytracer.hpp:25-36, material.hpp) — one normalisation per live lane, as in FP64
+    // ---- shade (raytracer.hpp:25-36, material.hpp), material-uniform as in the FP64 kernel: one
+    //      block of canonicals (float: one word each) for lambertian's vec3::random (3), the fuzzed
+    //      metal's factor and vector (4) and the dielectric's uniform (1, drawn speculatively and
+    //      given back on total internal reflection); one normalisation; one second square root
+    //      (the fuzzed metal's |vector|, the dielectric's sin(theta)).  Each lane's own operations
+    //      and their order are the reference's render<float>.
     bool ended = in_path && !alive;
     double L_r = 0, L_g = 0, L_b = 0;
     if (alive) {
       SphereMat m{};
       ykf::v3 p{0, 0, 0}, nrm{0, 0, 0};
       bool front = false;
-      ykf::v3 vn = d;
       if (hid >= 0) {
         const float4 sg = geo_f[hid];
         m = mat[hid];
@@ -1403,10 +1407,40 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
         const ykf::v3 outward = ykf::divs(ykf::sub(p, ykf::v3{sg.x, sg.y, sg.z}), (float)m.radius);
         front = ykf::dot(d, outward) < 0;
         nrm = front ? outward : ykf::neg(outward);
-        if (m.kind == YK_MATERIAL_LAMBERTIAN) vn = ykf::random_vec(g, -1.0f, 1.0f);
       }
+      const bool lamb = hid >= 0 && m.kind == YK_MATERIAL_LAMBERTIAN;
+      const bool fuzzy = hid >= 0 && m.kind == YK_MATERIAL_METAL && m.fuzz > 0;
+      const bool diel = hid >= 0 && m.kind == YK_MATERIAL_DIELECTRIC;
+      const bool spec = diel && ykd::rng_can_speculate(g);
+      const Gen saved = g;  // the dielectric's engine before its speculative draw
+      const uint32_t ncan = lamb ? 3u : (fuzzy ? 4u : (spec ? 1u : 0u));
+      float c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+      if (__ballot(ncan > 0 && !ykd::rng_lazy_ok(g, ncan)) == 0) {
+        if (ncan > 0) c0 = ykf::canonical<true>(g);
+        if (ncan > 1) c1 = ykf::canonical<true>(g);
+        if (ncan > 2) c2 = ykf::canonical<true>(g);
+        if (ncan > 3) c3 = ykf::canonical<true>(g);
+      } else {
+        if (ncan > 0) c0 = ykf::canonical(g);
+        if (ncan > 1) c1 = ykf::canonical(g);
+        if (ncan > 2) c2 = ykf::canonical(g);
+        if (ncan > 3) c3 = ykf::canonical(g);
+      }
+      // lambertian: vec3::random(-1, 1), x then y then z; fuzzed metal: the length factor first
+      const ykf::v3 rv = lamb ? ykf::v3{ykf::uniform_of(c0, -1.0f, 1.0f), ykf::uniform_of(c1, -1.0f, 1.0f),
+                                        ykf::uniform_of(c2, -1.0f, 1.0f)}
+                              : ykf::v3{ykf::uniform_of(c1, -1.0f, 1.0f), ykf::uniform_of(c2, -1.0f, 1.0f),
+                                        ykf::uniform_of(c3, -1.0f, 1.0f)};
+      const ykf::v3 vn = lamb ? rv : d;
       if (kCount) ++n_ncall;
       const ykf::v3 un = ykf::divs(vn, ykf::nsqrt(ykf::len2(vn), n_nit));
+      float ct = 0;  // dielectric: cos(theta) = min(dot(-unit, n), 1)
+      if (diel) {
+        ct = ykf::dot(ykf::neg(un), nrm);
+        if (!(ct < 1.0f)) ct = 1.0f;
+      }
+      float sq2 = 0;  // fuzzed metal: |random vector|; dielectric: sin(theta)
+      if (fuzzy || diel) sq2 = ykf::nsqrt(fuzzy ? ykf::len2(rv) : 1.0f - ct * ct, n_nit);
       if (hid < 0) {
         // sky: normalized(dir).y is a float; + 1.0 and the lerp are double (raytracer.hpp:35-36)
         const double t = ((double)un.y + 1.0) / 2;
@@ -1422,10 +1456,9 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
           if (ykf::near_zero(nd)) nd = nrm;
         } else if (m.kind == YK_MATERIAL_METAL) {
           nd = ykf::reflect(un, nrm);
-          if (m.fuzz > 0) {  // the length factor first, as in FP64
-            const float k = ykf::uniform(g, 0.01f, 0.99f);
-            ykf::v3 ru = ykf::random_vec(g, -1.0f, 1.0f);
-            ru = ykf::divs(ru, ykf::nsqrt(ykf::len2(ru), n_nit));
+          if (fuzzy) {
+            const float k = ykf::uniform_of(c0, 0.01f, 0.99f);
+            const ykf::v3 ru = ykf::divs(rv, sq2);
             nd = ykf::add(nd, ykf::mul(ykf::mul(ru, k), (float)m.fuzz));
           }
           scattered = ykf::dot(nd, nrm) > 0;
@@ -1433,11 +1466,14 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
           push = false;
           const float ior = (float)m.ior;
           const float ratio = front ? (1.0f / ior) : ior;
-          float ct = ykf::dot(ykf::neg(un), nrm);
-          if (!(ct < 1.0f)) ct = 1.0f;
-          const float sn = ykf::nsqrt(1.0f - ct * ct, n_nit);
-          const bool cannot = ratio * sn > 1.0f;
-          if (cannot || ykf::reflectance(ct, ratio) > f_uniform01(g)) {
+          const bool cannot = ratio * sq2 > 1.0f;
+          float u = 0;
+          if (cannot) {
+            if (spec) g = saved;  // `cannot || ...` never draws: give the word back
+          } else {
+            u = spec ? c0 : ykf::canonical(g);
+          }
+          if (cannot || ykf::reflectance(ct, ratio) > u) {
             nd = ykf::reflect(un, nrm);
           } else {
             const ykf::v3 perp = ykf::mul(ykf::add(un, ykf::mul(nrm, ct)), ratio);
