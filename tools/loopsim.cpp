@@ -123,6 +123,8 @@ int main(int argc, char** argv) {
   uint32_t seed = argc > 2 ? atoi(argv[2]) : 42;
   ykbvh::Options opt;
   if (argc > 3) opt.max_leaf = atoi(argv[3]);
+  if (const char* e = getenv("YKSIM_BINS")) opt.bins = atoi(e);
+  if (getenv("YKSIM_ALLAXES")) opt.all_axes = true;
   const double c_visit = argc > 4 ? atof(argv[4]) : 53, c_leaf = argc > 5 ? atof(argv[5]) : 20,
                c_disc = argc > 6 ? atof(argv[6]) : 40, c_trip = argc > 7 ? atof(argv[7]) : 10,
                frac = argc > 8 ? atof(argv[8]) : 1.0;

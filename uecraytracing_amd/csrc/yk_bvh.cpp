@@ -59,34 +59,43 @@ struct Builder {
     for (int k = 1; k < 3; ++k)
       if (cb.hi[k] - cb.lo[k] > cb.hi[axis] - cb.lo[axis]) axis = k;
     uint32_t mid = b + n / 2;
-    const double ext = cb.hi[axis] - cb.lo[axis];
+    double ext = cb.hi[axis] - cb.lo[axis];
     if (!median_only && ext > 0) {
       const int kBins = std::min(std::max(opt.bins, 2), 256);
-      std::vector<Box> bb(kBins);
-      std::vector<uint32_t> cnt(kBins, 0);
-      auto bin_of = [&](uint32_t s) {
-        int q = int((cent[3 * s + axis] - cb.lo[axis]) / ext * kBins);
+      // binned SAH over the longest centroid axis, or (opt.all_axes) the cheapest of the three
+      double best = INFINITY;
+      int best_q = -1, best_axis = axis;
+      for (int ax = 0; ax < 3; ++ax) {
+        if (!opt.all_axes && ax != axis) continue;
+        const double ex = cb.hi[ax] - cb.lo[ax];
+        if (!(ex > 0)) continue;
+        std::vector<Box> bb(kBins);
+        std::vector<uint32_t> cnt(kBins, 0);
+        for (uint32_t i = b; i < e; ++i) {
+          const uint32_t sp = idx[i];
+          const int q = std::min(std::max(int((cent[3 * sp + ax] - cb.lo[ax]) / ex * kBins), 0), kBins - 1);
+          bb[q].grow(sbox[sp]);
+          ++cnt[q];
+        }
+        for (int q = 1; q < kBins; ++q) {
+          Box l, r;
+          uint32_t nl = 0, nr = 0;
+          for (int t = 0; t < q; ++t) { l.grow(bb[t]); nl += cnt[t]; }
+          for (int t = q; t < kBins; ++t) { r.grow(bb[t]); nr += cnt[t]; }
+          if (!nl || !nr) continue;
+          const double cost = l.area() * nl + r.area() * nr;
+          if (cost < best) { best = cost; best_q = q; best_axis = ax; }
+        }
+      }
+      axis = best_axis;
+      ext = cb.hi[axis] - cb.lo[axis];
+      auto bin_of = [&](uint32_t sp) {
+        int q = int((cent[3 * sp + axis] - cb.lo[axis]) / ext * kBins);
         return std::min(std::max(q, 0), kBins - 1);
       };
-      for (uint32_t i = b; i < e; ++i) {
-        const int q = bin_of(idx[i]);
-        bb[q].grow(sbox[idx[i]]);
-        ++cnt[q];
-      }
-      double best = INFINITY;
-      int best_q = -1;
-      for (int q = 1; q < kBins; ++q) {
-        Box l, r;
-        uint32_t nl = 0, nr = 0;
-        for (int t = 0; t < q; ++t) { l.grow(bb[t]); nl += cnt[t]; }
-        for (int t = q; t < kBins; ++t) { r.grow(bb[t]); nr += cnt[t]; }
-        if (!nl || !nr) continue;
-        const double cost = l.area() * nl + r.area() * nr;
-        if (cost < best) { best = cost; best_q = q; }
-      }
       if (best_q > 0) {
         auto it = std::partition(idx.begin() + b, idx.begin() + e,
-                                 [&](uint32_t s) { return bin_of(s) < best_q; });
+                                 [&](uint32_t sp) { return bin_of(sp) < best_q; });
         mid = uint32_t(it - idx.begin());
       }
     }

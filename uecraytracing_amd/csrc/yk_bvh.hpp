@@ -81,6 +81,7 @@ struct Built {
 struct Options {
   uint32_t max_leaf = 2;  // spheres per leaf (<= 15); callers pick per kernel
   int bins = 16;          // SAH bins per split
+  bool all_axes = false;  // SAH over all three axes (false: the longest centroid axis only)
   double radius_grow = 0; // extra box growth per unit |radius| (FP32 trees: 2 kF32Cone)
   bool f32_big = false;   // FP32 trees: kF32BigGrow for spheres within kF32BigReach radii
 };
