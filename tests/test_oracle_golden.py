@@ -105,6 +105,31 @@ def test_newton_sqrt_one_step_from_ieee_sqrt():
             assert (r + s / r) / 2.0 == oracle_lib.newton_sqrt(s), s.hex()
 
 
+def test_newton_sqrt_f32_one_step_from_ieee_sqrt():
+    """The FP32 path's math::sqrt<float> for s in [2^-100, 2^100] (yk_device_f32.hpp nsqrt): ONE
+    step (r + s/r) * 0.5f from the correctly rounded r = sqrtf(s) equals the reference loop
+    (oracle's math.hpp:10-19 with T = float).  Here on every binade boundary +- 64 ulp and 3e5
+    random floats, in numpy float32 (IEEE, correctly rounded / and sqrt); tools/fsqrt_check.c ran
+    every float of the range."""
+    rng = np.random.default_rng(12)
+    vals = [np.ldexp(np.float32(1.0) + rng.random(300000, dtype=np.float32),
+                     rng.integers(-100, 100, 300000)).astype(np.float32)]
+    for k in range(-100, 101):
+        up = dn = np.float32(np.ldexp(np.float32(1.0), k))
+        edge = []
+        for _ in range(64):
+            edge += [up, dn]
+            up, dn = np.nextafter(up, np.float32(np.inf)), np.nextafter(dn, np.float32(0.0))
+        vals.append(np.array(edge, np.float32))
+    s = np.concatenate(vals).astype(np.float32)
+    s = s[(s >= np.float32(2.0 ** -100)) & (s <= np.float32(2.0 ** 100))]
+    r = np.sqrt(s)
+    one = ((r + s / r) * np.float32(0.5)).astype(np.float32)
+    want = oracle_lib.newton_sqrt_f32(s)
+    bad = np.nonzero(one.view(np.uint32) != want.view(np.uint32))[0]
+    assert bad.size == 0, s[bad[:5]]
+
+
 def test_newton_sqrt_kat():
     for x, y in golden_data.kat()["newton_sqrt"]:
         assert oracle_lib.newton_sqrt(float.fromhex(x)).hex() == float.fromhex(y).hex(), x

@@ -653,7 +653,8 @@ void yk_render_persistent(KernelArgs ka) {
       double uc = 0, vc = 0, px = 0, py = 0;
       bool pre = false;
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
-        const StartRec r = ((const StartRec*)ka.start)[slot];
+        // (YK_ABLATE & 128, timing only: records from a 1024-slot window, always L2-resident)
+        const StartRec r = ((const StartRec*)ka.start)[(YK_ABLATE & 128) ? (slot & 1023u) : slot];
         pre = r.j != kNoStart;
         if (pre) {
           g.seed = seed;
