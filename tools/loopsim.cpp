@@ -9,7 +9,12 @@
 // line): visit, leaf discriminant, the disc >= 0 tail, loop overhead.
 //   build: g++ -O2 -std=c++17 -Iinclude tools/loopsim.cpp uecraytracing_amd/csrc/yk_bvh.cpp \
 //          uecraytracing_amd/csrc/yk_host.cpp -o /tmp/loopsim
-//   run:   /tmp/loopsim final 42 [leaf] [c_visit c_leaf c_disc c_trip]
+//   run:   /tmp/loopsim final 42 [leaf] [c_visit c_leaf c_disc c_trip frac]
+//   env:   YKSIM_BINS=n (SAH bins), YKSIM_ALLAXES=1 (SAH over all axes), YKSIM_WIDTH=n (an n-wide
+//          tree, n <= 8, in the if/else loop: wave-level visit and leaf blocks per segment)
+// The pool models (a wave-wide LIFO of (ray, node) pairs) and the speculative variant count wave
+// trips and blocks only; their measured kernels were slower or neutral, because the
+// node loop is bound by LDS latency and trip count, which these weights do not price.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -118,6 +123,48 @@ struct Model {
   }
 };
 
+// ---- N-wide model (YKSIM_WIDTH=N, N <= 8): the binary tree collapsed greedily (largest surface
+// area first, as ykbvh::wide_nodes) to N slots per node; the same if/else loop per lane
+struct WideN {
+  float lo[8][3], hi[8][3];
+  int32_t code[8];  // >= 0: node index, < 0: leaf code
+  int n;
+};
+static void collapse_n(const ykbvh::Built& b, std::vector<WideN>& out, int32_t code, int width) {
+  struct E { float lo[3], hi[3]; int32_t code; };
+  auto ent = [&](const ykbvh::Node& nd, int k) {
+    return E{{nd.lo_x[k], nd.lo_y[k], nd.lo_z[k]}, {nd.hi_x[k], nd.hi_y[k], nd.hi_z[k]}, nd.child[k]};
+  };
+  std::vector<E> ents = {ent(b.nodes[code], 0), ent(b.nodes[code], 1)};
+  auto area = [](const E& e) {
+    float dx = e.hi[0] - e.lo[0], dy = e.hi[1] - e.lo[1], dz = e.hi[2] - e.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  while ((int)ents.size() < width) {
+    int best = -1;
+    for (size_t i = 0; i < ents.size(); ++i)
+      if (ents[i].code >= 0 && (best < 0 || area(ents[i]) > area(ents[best]))) best = (int)i;
+    if (best < 0) break;
+    const ykbvh::Node& c = b.nodes[ents[best].code];
+    ents[best] = ent(c, 0);
+    ents.insert(ents.begin() + best + 1, ent(c, 1));
+  }
+  const size_t me = out.size();
+  out.push_back(WideN{});
+  WideN w{};
+  w.n = (int)ents.size();
+  for (int k = 0; k < w.n; ++k) {
+    for (int a = 0; a < 3; ++a) { w.lo[k][a] = ents[k].lo[a]; w.hi[k][a] = ents[k].hi[a]; }
+    if (ents[k].code >= 0) {
+      w.code[k] = (int32_t)out.size();
+      collapse_n(b, out, ents[k].code, width);
+    } else {
+      w.code[k] = ents[k].code;
+    }
+  }
+  out[me] = w;
+}
+
 int main(int argc, char** argv) {
   const char* scene = argc > 1 ? argv[1] : "final";
   uint32_t seed = argc > 2 ? atoi(argv[2]) : 42;
@@ -194,6 +241,63 @@ int main(int argc, char** argv) {
 
   printf("%s n=%u leaf<=%u wide nodes %zu depth %u | %zu segments | weights visit %.0f leaf %.0f disc %.0f trip %.0f\n",
          scene, n, opt.max_leaf, M.wide.size(), wd, seg.size(), c_visit, c_leaf, c_disc, c_trip);
+  if (const char* we = getenv("YKSIM_WIDTH")) {
+    const int width = atoi(we);
+    std::vector<WideN> wn;
+    collapse_n(b, wn, b.root, width);
+    double vb = 0, lb = 0, lv = 0, ll = 0;
+    size_t nw = 0;
+    for (size_t g = 0; g + 64 <= idx.size(); g += 64, ++nw) {
+      struct L { V o, d; double a, ustar = INFINITY; float ix, iy, iz, uf = INFINITY; std::vector<int32_t> st; int32_t node = 0; bool done = false; };
+      std::vector<L> ls(64);
+      for (int k = 0; k < 64; ++k) {
+        L& x = ls[k];
+        x.o = seg[idx[g + k]].first; x.d = seg[idx[g + k]].second; x.a = dot(x.d, x.d);
+        x.ix = rcp((float)x.d.x); x.iy = rcp((float)x.d.y); x.iz = rcp((float)x.d.z);
+      }
+      for (;;) {
+        bool av = false, al = false, act = false;
+        for (auto& x : ls) {
+          if (x.done) continue;
+          act = true;
+          if (x.node >= 0) {
+            av = true; ++lv;
+            const WideN& w = wn[x.node];
+            int last = -1;
+            bool hk[8];
+            for (int k = 0; k < w.n; ++k) {
+              const float i3[3] = {x.ix, x.iy, x.iz};
+              const double o3[3] = {x.o.x, x.o.y, x.o.z};
+              float tn = 0.001f, tf = x.uf;
+              for (int a = 0; a < 3; ++a) {
+                float t0 = (w.lo[k][a] - (float)o3[a]) * i3[a], t1 = (w.hi[k][a] - (float)o3[a]) * i3[a];
+                tn = std::max(tn, std::min(t0, t1)); tf = std::min(tf, std::max(t0, t1));
+              }
+              hk[k] = tn <= tf * (1 + 0x1p-17f);
+              if (hk[k]) last = k;
+            }
+            if (last < 0) {
+              if (x.st.empty()) x.done = true; else { x.node = x.st.back(); x.st.pop_back(); }
+            } else {
+              for (int k = 0; k < last; ++k) if (hk[k]) x.st.push_back(w.code[k]);
+              x.node = w.code[last];
+            }
+          } else {
+            al = true;
+            Lane tmp; tmp.o = x.o; tmp.d = x.d; tmp.a = x.a; tmp.ustar = x.ustar; tmp.uf = x.uf;
+            auto [cnt, dp] = M.leaf(tmp, x.node);
+            (void)dp; ll += cnt;
+            x.ustar = tmp.ustar; x.uf = tmp.uf;
+            if (x.st.empty()) x.done = true; else { x.node = x.st.back(); x.st.pop_back(); }
+          }
+        }
+        if (!act) break;
+        vb += av; lb += al;
+      }
+    }
+    printf("width %d: %zu nodes | per wave-segment: visit blocks %.1f, leaf blocks %.1f | per lane: visits %.2f, leaf tests %.2f\n",
+           width, wn.size(), vb / nw, lb / nw, lv / (64.0 * nw), ll / (64.0 * nw));
+  }
   // ---- wave work-pool models: one LIFO of (ray, node) pairs per wave, 64 pairs per trip
   // pool 0: nodes and leaves mixed in the pool; pool 1: leaves go to a list tested 64 at a time
   // (when it holds 64, or the node pool is empty)

@@ -262,7 +262,6 @@ __device__ __forceinline__ void mt_walk397xn(uint32_t (&x)[N]) {
   }
 #endif
 }
-__device__ __forceinline__ void mt_walk397x4(uint32_t (&x)[4]) { mt_walk397xn<4>(x); }
 
 // The rare path: the real engine in global scratch (seed :69-81, M_gen_rand :114-131).
 // Out of line and by value so the hot path keeps the lane's cursors in registers.
