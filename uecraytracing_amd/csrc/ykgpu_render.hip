@@ -761,9 +761,10 @@ void yk_render_persistent(KernelArgs ka) {
         // candidate lower bounds kept as floats rounded down, compared with ustar_f (>= U*):
         // both only ever keep MORE candidates than the double comparison would
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-        // a VGPR, not a bool: a bool carried round the traversal loop lives in a lane mask that
-        // every divergent exit has to merge (-3.4% render time as an integer)
-        uint32_t overflow = 0;
+        // overflow of the stack or of the candidate list is recorded as nc = 5, not as a flag of
+        // its own: a bool carried round the traversal loop lives in a lane mask that every
+        // divergent exit has to merge (-3.4% as a bool), an integer flag is one more loop-carried
+        // register (nc = 5 instead: -0.8%)
         int32_t node = ka.bvh_root;
 #if YK_WIDE
         int32_t* top = stk;  // this lane's traversal stack top (entries kBlk words apart)
@@ -818,10 +819,11 @@ void yk_render_persistent(KernelArgs ka) {
               top += (hk[1] && (hk[2] || hk[3])) ? kBlk : 0;
               *top = ch.z;
               top += (hk[2] && hk[3]) ? kBlk : 0;
-              if (top > stk_cap) {  // stack full: abandon, the exact linear scan decides
-                overflow = true;
-                top = stk;
-                node = ykbvh::kEmptyLeaf;
+              // stack full: the top stays at the capacity (the pushes above it are lost and the
+              // rest of this traversal is void) and nc = 5 marks the lane for the exact linear scan
+              if (top > stk_cap) {
+                top = stk + ka.stack_cap * kBlk;
+                nc = 5;
               }
               continue;
             }
@@ -903,7 +905,7 @@ void yk_render_persistent(KernelArgs ka) {
                 YK_CAND_SET(nc, id, __double2float_rd(lb));
                 ++nc;
               } else {
-                overflow = true;
+                nc = 5;  // the list is full: overflow (the exact linear scan decides)
               }
             }
             YK_STAMP(6);  // this leaf
@@ -919,7 +921,7 @@ void yk_render_persistent(KernelArgs ka) {
 #endif
         }
         YK_STAMP(2);
-        if (overflow) {
+        if (nc > 4) {
           linear = true;
         } else {
           // exact evaluation of the survivors; the roots' divisor a is the same for every
