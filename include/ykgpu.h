@@ -146,7 +146,7 @@ typedef struct yk_render_params {
 
 typedef struct yk_render_stats {
   double kernel_ms;        /* path-tracing kernel, summed over its launches (HIP events on
-                              the render stream around each launch; consecutive launches
+                              the render streams around each launch; consecutive launches
                               overlap, so this can exceed the call)                      */
   double resolve_ms;       /* ordered per-pixel sum + to_color3b kernel, summed           */
   double total_ms;         /* whole call: host wall clock for ykgpu_render / _sums (with
@@ -199,8 +199,12 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
  * caller-owned host buffer of row_count * W * 3 bytes laid out like image_t. */
 int ykgpu_render(ykgpu_context* ctx, const yk_render_params* params, uint8_t* rgb_host);
 
-/* Same, into device memory (row_count * W * 3 bytes on ctx's device), enqueued on `stream`
- * (a hipStream_t; NULL = the context's own stream).  Does not synchronise. */
+/* Same, into device memory (row_count * W * 3 bytes on ctx's device), ordered on `stream`
+ * (a hipStream_t; NULL = the context's own stream): the render starts after the work already
+ * queued on `stream` and the image is complete for the work queued after it.  Internally the
+ * kernels run on the context's own streams (render launches at the device's top stream
+ * priority, the seed walks and the reduces below it) joined to `stream` by events.  Does not
+ * synchronise. */
 int ykgpu_render_async(ykgpu_context* ctx, const yk_render_params* params, void* rgb_device,
                        void* stream);
 
