@@ -758,8 +758,9 @@ void yk_render_persistent(KernelArgs ka) {
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
         float ustar_f = INFINITY;  // >= ustar * (1 + 2^-18)
         uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-        // candidate lower bounds kept as floats rounded down, compared with ustar_f (>= U*):
-        // both only ever keep MORE candidates than the double comparison would
+        // candidate lower bounds kept as floats RN(L), compared with ustar_f >= RN(U*): by
+        // monotone rounding (all bounds >= 0) L <= U* implies RN(L) <= ustar_f, so the float
+        // comparison only ever keeps MORE candidates than the double comparison would
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
         // overflow of the stack or of the candidate list is recorded as nc = 5, not as a flag of
         // its own: a bool carried round the traversal loop lives in a lane mask that every
@@ -902,7 +903,13 @@ void yk_render_persistent(KernelArgs ka) {
                 nc = m2;
               }
               if (nc < 4) {
-                YK_CAND_SET(nc, id, __double2float_rd(lb));
+                // shifted in at entry 0 — straight-line moves instead of a branch per list
+                // position (evaluation order never matters: min root, later index on ties).
+                // RN(lb), not rounded down: t_min >= 0 (checked by the host) makes every lb and
+                // U* >= 0, and lb <= U* implies RN(lb) <= RN(U*) <= ustar_f (monotone rounding),
+                // so the list still keeps every sphere that can be the minimum
+                c3 = c2, l3 = l2, c2 = c1, l2 = l1, c1 = c0, l1 = l0;
+                c0 = id, l0 = (float)lb;
                 ++nc;
               } else {
                 nc = 5;  // the list is full: overflow (the exact linear scan decides)
