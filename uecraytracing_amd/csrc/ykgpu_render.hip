@@ -721,7 +721,23 @@ void yk_render_persistent(KernelArgs ka) {
         // t = lo*(1/d) - o*(1/d): error relative 2^-22 plus an origin perturbation of
         // 2^-23|o| (< delta/4), inside the culling contract of yk_bvh.hpp.  This is culling
         // arithmetic only, so explicit FMAs are fine here.
-        const float ix = safe_rcp((float)d.x), iy = safe_rcp((float)d.y), iz = safe_rcp((float)d.z);
+        // 1/d from v_rcp_f32 (1 ulp): with d's rounding to float and the FMA's rounding the
+        // slab distances stay within the 2^-22 relative error the culling contract assumes
+        // (2^-24 + 2^-23 + 2^-24).  Components outside [1e-30, 1e30] (never seen) take the
+        // correctly rounded division for the whole wave.
+        const float dxf = (float)d.x, dyf = (float)d.y, dzf = (float)d.z;
+        const float dmin = fminf(fminf(fabsf(dxf), fabsf(dyf)), fabsf(dzf));
+        const float dmax = fmaxf(fmaxf(fabsf(dxf), fabsf(dyf)), fabsf(dzf));
+        float ix, iy, iz;
+        if (__ballot(!(dmin > 1e-30f && dmax < 1e30f)) == 0) {
+          ix = __builtin_amdgcn_rcpf(dxf);
+          iy = __builtin_amdgcn_rcpf(dyf);
+          iz = __builtin_amdgcn_rcpf(dzf);
+        } else {
+          ix = safe_rcp(dxf);
+          iy = safe_rcp(dyf);
+          iz = safe_rcp(dzf);
+        }
         const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
 #if YK_WIDE
         // this ray's (near x4, far x4) plane quads inside a WideNode (yk_bvh.hpp), as base
