@@ -161,6 +161,7 @@ struct KernelArgs {
   const void* __restrict__ start;      // StartRec per sample slot (FP64 mt19937 kernel)
   double t_min;
   double inv_w, inv_h;  // RN(1/W), RN(1/H) for the camera's exact divisions (div_markstein)
+  double w_d, h_d;      // W, H as doubles (kernel arguments: no loop-hoisted conversion to hold)
   double origin_bound;  // |o|_inf beyond which the BVH's float culling is not proven sound
   int32_t bvh_root;
   uint32_t n_nodes;
@@ -634,9 +635,22 @@ void yk_render_persistent(KernelArgs ka) {
     // ---- start sample s of the pixel: seed, jitter, camera ray (source.cpp:154-165) ------
     bool start = !in_path;
     uint32_t qpix = 0;
+    // the slot's pixel and (mt19937) its StartRec issued together and waited for once: tested
+    // one after the other they cost three dependent memory round trips per sample start (the
+    // record's j, then its other words under the test).  Every slot of the launch, padded ones
+    // included, has a record, so the read is in bounds.
+    uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0};
     if (start) {
       const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
       qpix = ka.order[slot - sl * ka.npix_slots];
+      if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
+        const uint4* rp = (const uint4*)ka.start + 3u * ((YK_ABLATE & 128) ? (slot & 1023u) : slot);
+        rq0 = rp[0];
+        rq1 = rp[1];
+        rq2 = rp[2];
+        asm volatile("" ::"v"(rq0.x), "v"(rq0.y), "v"(rq0.z), "v"(rq0.w), "v"(rq1.x), "v"(rq1.y),
+                     "v"(rq1.z), "v"(rq1.w), "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(qpix));
+      }
       start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
     if (start) {
@@ -654,7 +668,10 @@ void yk_render_persistent(KernelArgs ka) {
       bool pre = false;
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
         // (YK_ABLATE & 128, timing only: records from a 1024-slot window, always L2-resident)
-        const StartRec r = ((const StartRec*)ka.start)[(YK_ABLATE & 128) ? (slot & 1023u) : slot];
+        StartRec r;  // (loaded above with the pixel)
+        __builtin_memcpy((char*)&r, &rq0, 16);
+        __builtin_memcpy((char*)&r + 16, &rq1, 16);
+        __builtin_memcpy((char*)&r + 32, &rq2, 16);
         pre = r.j != kNoStart;
         if (pre) {
           g.seed = seed;
@@ -680,8 +697,8 @@ void yk_render_persistent(KernelArgs ka) {
         }
       }
       // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
-      const double u = ykd::div_markstein((double)x + ykd::uniform_of(uc, 0, 1), (double)ka.W, ka.inv_w);
-      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform_of(vc, 0, 1), (double)ka.H, ka.inv_h);
+      const double u = ykd::div_markstein((double)x + ykd::uniform_of(uc, 0, 1), ka.w_d, ka.inv_w);
+      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform_of(vc, 0, 1), ka.h_d, ka.inv_h);
       // camera::get_ray (camera.hpp:29-32): llc + u*horizontal + v*vertical (- origin)
       const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
       const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
@@ -884,6 +901,10 @@ void yk_render_persistent(KernelArgs ka) {
 #endif
             for (uint32_t k = 0; k < cnt; ++k) {
               const SphereGeo sg = leaf_geo[first + k];
+              // the tuple index read with the geometry: its latency then hides under the
+              // discriminant instead of following the bounds on the insert path
+              const uint32_t id = leaf_ids[first + k];
+              asm volatile("" ::"v"(id));
               ++n_test;
               // the reference's discriminant, bit for bit (sphere.hpp:29-34)
               const v3 oc = {o.x - sg.cx, o.y - sg.cy, o.z - sg.cz};
@@ -907,7 +928,6 @@ void yk_render_persistent(KernelArgs ka) {
                 ustar = ub;
                 ustar_f = (float)ub * (1.0f + 0x1p-18f);
               }
-              const uint32_t id = leaf_ids[first + k];
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
                 uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
@@ -1907,6 +1927,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.origin_bound = tree.origin_bound;
   ka.inv_w = 1.0 / (double)ka.W;
   ka.inv_h = 1.0 / (double)ka.H;
+  ka.w_d = (double)ka.W;
+  ka.h_d = (double)ka.H;
   ka.bvh_root = tree.root;
   ka.n_nodes = tree.n_nodes;
   ka.lds_geo_off = tree.geo_off;
