@@ -121,7 +121,7 @@ def main():
     import uecraytracing_amd as yk
     from uecraytracing_amd import flops
     from uecraytracing_amd.records import image_height_for, make_params
-    from uecraytracing_amd.tiles import TileGather, tile_rows
+    from uecraytracing_amd.tiles import BAND_LOG2, TileGather, tile_rows
 
     # one process per GPU; YK_BENCH_BACKEND=gloo (rehearsal only) lets several ranks share a GPU
     backend = os.environ.get("YK_BENCH_BACKEND", "nccl")
@@ -251,7 +251,8 @@ def main():
                         f"seed0 {args.seed0}, mt19937 + FP64 bit-exact",
             "image": f"{W}x{H}", "spp": spp, "max_depth": depth, "spheres": len(spheres),
             "scene_file": os.path.relpath(scene_file, ROOT) if scene_file else None,
-            "partition": f"cyclic 8-row bands over {world} GPU(s), RCCL gather to rank 0",
+            "partition": f"rows dealt cyclically in bands of {1 << BAND_LOG2} over {world} GPU(s), "
+                         f"RCCL gather to rank 0",
         },
         "scene_upload_ms": round(scene_upload_ms, 3),
         "value_incl_scene_upload": round(total_samples * args.steps

@@ -2,10 +2,12 @@
 
 Every sample's random stream depends only on (y, x, s) (source.cpp:154-158) and every pixel is
 independent, so any partition of the rows renders byte-identical pixels.  Rows are dealt in
-BANDS of 2^band_log2 consecutive rows (8 by default), band b → rank b mod N: cyclic dealing
-spreads cheap sky rows and expensive ground rows evenly, and whole bands keep the pixels a wave
-starts together adjacent in the image (single rows dealt cyclically cost 9-17% more per sample
-on 2-8 GPUs: the rays of a wave spread over N times the image area).  Each rank's tile is a
+BANDS of 2^band_log2 consecutive rows, band b → rank b mod N: cyclic dealing spreads cheap sky
+rows and expensive ground rows evenly.  The default is single rows (band_log2 = 0): with 8-row
+bands rank r's rows sit 8r rows lower in every period, and on the final round-2 kernel the
+slowest of 8 ranks took 29.2 ms against 27.5 ms with single rows, 101.2 against 97.6 ms at
+2 ranks (profiles/r02bq_rank_tiles, profiles/r02br_rank_tiles; the per-sample cost of single
+rows, 9-17% at round 1, no longer shows).  Each rank's tile is a
 contiguous uint8[rows_max, W, 3] buffer in HBM (padded to the largest tile so the collective
 moves equal-sized buffers), the tiles are gathered to rank 0 with one collective (RCCL over xGMI
 with backend 'nccl'; 'gloo' on CPU tensors in the tests), and rank 0 de-interleaves them with one
@@ -13,7 +15,7 @@ index_select.
 """
 from __future__ import annotations
 
-BAND_LOG2 = 3
+BAND_LOG2 = 0
 
 
 def tile_rows(rank: int, world: int, height: int, band_log2: int = BAND_LOG2):
