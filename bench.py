@@ -32,7 +32,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/sec at 1920x1080x512spp (~500 spheres); per-pixel RMSE vs CPU"
-FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= FP32 vector 157.3 TF / 2, MI355X_MICROARCH.md)
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 SPHERE_RECORD_BYTES = 80      # yk_sphere (include/ykgpu.h): the scene a workgroup stages once
 
@@ -86,6 +85,77 @@ def pmc_facts(workload=None):
     return {k: rec[k] for k in keep if k in rec}
 
 
+def other_configs(ren, stream, seed0, nthreads, peak_tf):
+    """BASELINE configs 4 and 5 on this GPU, after the contract line's timed region (rank 0, N=1):
+    config 5 = 1920x1080x4096, max_depth 200, the dielectric-heavy glass scene, whole frame (the
+    active-ray compaction stress); config 4 = 3840x2160x1024 on the final scene, rank 0's tile of
+    the 8-GPU split (every 8th row from 0: what one GPU renders in the driver's 8-GPU run).  Each:
+    one warm call, one timed call (HIP events around the call on the bench stream), the roofline
+    from a counting call, and the timed image's rows compared with the CPU oracle."""
+    import numpy as np
+    import torch
+
+    import uecraytracing_amd as yk
+    from uecraytracing_amd import flops
+    from uecraytracing_amd.records import image_height_for, make_params
+    from uecraytracing_amd.tiles import tile_rows
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+
+    out = {}
+    cases = (("config5", "glass", 1920, 4096, 200, None, (17, 1061)),
+             ("config4_rank0_of_8", "final", 3840, 1024, 50, (0, 8), (0, 134)))
+    for name, scene, W, spp, depth, split, cmp_rows in cases:
+        scene_file = os.path.join(yk.SCENE_DIR, f"{scene}_seed42.yks")
+        spheres, cam = yk.read_scene(scene_file)
+        ren.set_scene(spheres, cam)
+        H = image_height_for(W)
+        rows = tile_rows(split[0], split[1], H) if split else (0, H, 1, 0)
+        tile = torch.empty((rows[1], W, 3), dtype=torch.uint8, device=torch.device("cuda", ren.device))
+        p = make_params(W, H, spp, depth, seed0, rows=rows, flags=0)
+        with torch.cuda.stream(stream):
+            ren.render_async(p, tile.data_ptr(), stream.cuda_stream)  # warm call (allocations)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            ren.render_async(p, tile.data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        tst = ren.stats()
+        img = tile.cpu().numpy()
+        ren.render_async(make_params(W, H, spp, depth, seed0, rows=rows, flags=1), tile.data_ptr(),
+                         stream.cuda_stream)
+        torch.cuda.synchronize()
+        st = ren.stats()
+        n = rows[1] * W * spp
+        launches = max(1, tst["launches"])
+        launch_ms = tst["render_busy_ms"] / launches
+        alg = flops.algorithmic(st)
+        ach = alg / launches / (launch_ms * 1e-3) / 1e12
+        # parity: tile rows cmp_rows (their image rows y) against the oracle at full spp
+        ys = [rows[0] + t * rows[2] for t in cmp_rows]
+        cpu = np.concatenate([oracle_lib.render(spheres, cam, make_params(W, H, spp, depth, seed0, rows=(y, 1, 1)),
+                                                nthreads=nthreads)[0] for y in ys])
+        gpu = img[list(cmp_rows)]
+        out[name] = {
+            "workload": f"{W}x{H}x{spp}spp, max_depth {depth}, {os.path.relpath(scene_file, ROOT)} "
+                        f"({len(spheres)} spheres), seed0 {seed0}, mt19937 + FP64"
+                        + (f", rows {rows[0]}::{rows[2]} ({rows[1]} rows = rank {split[0]} of {split[1]})" if split else ""),
+            "value": round(n / (ms * 1e-3) / 1e6, 3), "unit": "Msamples/s", "ms": round(ms, 3),
+            "samples": n, "launches": launches,
+            "roofline": {"bound": "valu", "achieved": round(ach, 4), "peak": peak_tf, "unit": "TFLOP/s",
+                         "frac": round(ach / peak_tf, 5), "launch_ms": round(launch_ms, 4),
+                         "algorithmic_flops_per_launch": round(alg / launches)},
+            "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
+            "mt_fallback_samples": st["mt_fallbacks"],
+            "device_bytes": tst["device_bytes"],
+            "parity_vs_cpu": {"image_rows_compared": ys, "bytes_differing": int((gpu != cpu).sum()),
+                              "max_abs_levels": int(np.abs(gpu.astype(int) - cpu.astype(int)).max())},
+        }
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +174,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-modes", action="store_true",
                     help="skip the one-call timings of the FP32 and xor128 modes (rank 0, N=1)")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the BASELINE config 4 / 5 measurements (rank 0, N=1)")
     return ap.parse_args()
 
 
@@ -212,6 +284,8 @@ def main():
     # overlap: the per-launch duration is the UNION of the spans / launches, never their sum.
     busy_ms = tst["render_busy_ms"]
     launch_ms = busy_ms / launches
+    # the FP64 VALU peak measured on this chip (tools/ubench.hip → profiles/r03_ubench.jsonl)
+    peak_tf, peak_ev = flops.fp64_valu_peak()
     alg = flops.algorithmic(st)       # FP64 flops of the reference's expressions, per step
     impl = flops.implementation(st)   # counter-weighted FP64 operations the kernel executes
     achieved_tf = alg / launches / (launch_ms * 1e-3) / 1e12
@@ -262,9 +336,11 @@ def main():
         "roofline": {
             "bound": "valu",
             "achieved": round(achieved_tf, 4),
-            "peak": FP64_VALU_PEAK_TFLOPS,
+            "peak": peak_tf,
             "unit": "TFLOP/s",
-            "frac": round(achieved_tf / FP64_VALU_PEAK_TFLOPS, 5),
+            "frac": round(achieved_tf / peak_tf, 5),
+            "peak_evidence": peak_ev,
+            "frac_of_spec": round(achieved_tf / flops.SPEC_FP64_VALU_TFLOPS, 5),
             "traffic": traffic,
             "kernel": "yk_render_persistent",
             "launches_per_step": launches,
@@ -276,7 +352,7 @@ def main():
             "implementation": {
                 "flops_per_launch": round(impl / launches),
                 "achieved": round(impl_tf, 4),
-                "frac": round(impl_tf / FP64_VALU_PEAK_TFLOPS, 5),
+                "frac": round(impl_tf / peak_tf, 5),
                 "note": "FP64 operations the kernel executes (divisions as rcp+FMA sequences, "
                         "math::sqrt's start and steps, the BVH's root bounds), weighted as "
                         "SQ_INSTS_VALU_FLOPS_FP64 weighs them (uecraytracing_amd/flops.py)",
@@ -286,6 +362,8 @@ def main():
             "hbm": {"algorithmic_bytes_per_launch": round(hbm_step / launches),
                     "achieved": round(hbm_gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 7), "traffic": traffic,
+                    "traffic_over_algorithmic": round(traffic / (hbm_step / launches), 1) if traffic else None,
+                    "device_bytes": tst["device_bytes"],
                     "algorithmic": f"SURVEY §8(d): the RGB8 image ({rows_mine * W * 3} B) once per "
                                    f"step + the scene ({scene_bytes} B) once per workgroup "
                                    f"({tst['grid_blocks']} per launch); traffic = PMC FETCH_SIZE x2 + "
@@ -389,6 +467,9 @@ def main():
             modes[name] = {"value": round(total_samples / dt / 1e6, 3), "unit": "Msamples/s",
                            "ms": round(dt * 1e3, 3)}
         result["modes"] = modes
+
+    if rank == 0 and world == 1 and not args.no_configs:
+        result["configs"] = other_configs(ren, stream, args.seed0, args.cpu_threads or usable_cpus()[0], peak_tf)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -9,12 +9,15 @@
 //   * the reference's yk/hittable_list.hpp + yk/sphere.hpp + yk/material.hpp + yk/camera.hpp
 // — i.e. the reference's source.cpp can hand its world to the GPU unchanged.
 //
-// Then ykgpu::renderer runs the render loop of source.cpp:122-172 on the device and returns
-// the image_t bytes (source.cpp:70-71: row-major, row 0 at the top, RGB interleaved).
+// Then ykgpu::renderer runs the render loop of source.cpp:122-172 on the device — or on several:
+// a device list (ykgpu_group_*, include/ykgpu.h; from the environment with devices_from_env())
+// deals the image's rows over them — and returns the image_t bytes (source.cpp:70-71:
+// row-major, row 0 at the top, RGB interleaved).
 #pragma once
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <iomanip>
@@ -154,24 +157,76 @@ struct render_options {
   double t_min = 0.001;                    // raytracer.hpp:27
 };
 
-// One device context: the render loop of source.cpp:122-172 on the GPU.
+// The devices a drop-in render uses, from the environment: YKGPU_DEVICES unset or empty → {0};
+// "all" → every device of the node (ykgpu_device_count); otherwise a comma-separated list of
+// device indices, repeats allowed ("0,1,2,3,4,5,6,7"; "0,0,0" runs three contexts on device 0).
+inline std::vector<int> devices_from_env(const char* var = "YKGPU_DEVICES") {
+  const char* e = std::getenv(var);
+  std::vector<int> d;
+  if (!e || !*e) return {0};
+  const std::string v = e;
+  if (v == "all") {
+    int n = 0;
+    check(ykgpu_device_count(&n), "ykgpu_device_count");
+    for (int k = 0; k < n; ++k) d.push_back(k);
+    if (d.empty()) throw error(YK_ERR_DEVICE, "YKGPU_DEVICES=all: no device");
+    return d;
+  }
+  size_t i = 0;
+  while (i < v.size()) {
+    size_t used = 0;
+    int k = 0;
+    try {
+      k = std::stoi(v.substr(i), &used);
+    } catch (const std::exception&) {
+      used = 0;
+    }
+    if (used == 0 || k < 0) throw error(YK_ERR_INVALID, std::string(var) + ": not a device list: " + v);
+    d.push_back(k);
+    i += used;
+    if (i < v.size() && v[i] != ',') throw error(YK_ERR_INVALID, std::string(var) + ": not a device list: " + v);
+    if (i < v.size()) ++i;
+  }
+  if (d.empty()) throw error(YK_ERR_INVALID, std::string(var) + ": empty device list");
+  return d;
+}
+
+// The render loop of source.cpp:122-172 on the GPU: one device context, or — given several
+// devices — a group of contexts over which the image's rows are dealt (tile row t → entry t mod k).
+// Tracing (-l 3) always runs on one context of the first device.
 class renderer {
  public:
-  explicit renderer(int device = 0) { check(ykgpu_context_create(device, &ctx_), "ykgpu_context_create"); }
-  ~renderer() { ykgpu_context_destroy(ctx_); }
+  explicit renderer(int device = 0) : devices_{device} { check(ykgpu_context_create(device, &ctx_), "ykgpu_context_create"); }
+  explicit renderer(const std::vector<int>& devices) : devices_(devices) {
+    if (devices_.empty()) throw error(YK_ERR_INVALID, "empty device list");
+    if (devices_.size() == 1)
+      check(ykgpu_context_create(devices_[0], &ctx_), "ykgpu_context_create");
+    else
+      check(ykgpu_group_create(devices_.data(), (uint32_t)devices_.size(), &group_), "ykgpu_group_create");
+  }
+  ~renderer() {
+    ykgpu_group_destroy(group_);
+    ykgpu_context_destroy(ctx_);
+  }
   renderer(const renderer&) = delete;
   renderer& operator=(const renderer&) = delete;
 
+  const std::vector<int>& devices() const { return devices_; }
+
   template <class World, class Cam>
   void set_scene(const World& world, const Cam& cam) {
-    const std::vector<yk_sphere> s = flatten(world);
-    const yk_camera c = camera_record(cam);
-    check(ykgpu_set_scene(ctx_, s.data(), (uint32_t)s.size(), &c), "ykgpu_set_scene");
+    set_records(flatten(world), camera_record(cam));
   }
 
   // already-flattened records (e.g. yk_scene_build output)
   void set_records(const std::vector<yk_sphere>& s, const yk_camera& c) {
-    check(ykgpu_set_scene(ctx_, s.data(), (uint32_t)s.size(), &c), "ykgpu_set_scene");
+    if (group_)
+      check(ykgpu_group_set_scene(group_, s.data(), (uint32_t)s.size(), &c), "ykgpu_group_set_scene");
+    else
+      check(ykgpu_set_scene(ctx_, s.data(), (uint32_t)s.size(), &c), "ykgpu_set_scene");
+    spheres_ = s;
+    cam_ = c;
+    ctx_scene_ = !group_;
   }
 
   // image_t bytes of the whole image: W*H*3, row 0 at the top (source.cpp:70-71,224-226)
@@ -186,7 +241,10 @@ class renderer {
                               uint32_t seed0, const render_options& o) {
     const yk_render_params p = params(width, height, spp, max_depth, seed0, o);
     std::vector<uint8_t> img((size_t)width * height * 3);
-    check(ykgpu_render(ctx_, &p, img.data()), "ykgpu_render");
+    if (group_)
+      check(ykgpu_group_render(group_, &p, img.data()), "ykgpu_group_render");
+    else
+      check(ykgpu_render(ctx_, &p, img.data()), "ykgpu_render");
     return img;
   }
 
@@ -222,6 +280,7 @@ class renderer {
     const size_t n = (size_t)rows * width * spp;
     rays.assign(n * max_rays * 6, 0.0);
     counts.assign(n, 0);
+    trace_context();
     check(ykgpu_render_trace(ctx_, &p, max_rays, rays.data(), counts.data()), "ykgpu_render_trace");
   }
 
@@ -263,14 +322,32 @@ class renderer {
     }
   }
 
+  // the last render's statistics (a group: the whole call, include/ykgpu.h)
   yk_render_stats stats() {
     yk_render_stats s;
-    check(ykgpu_get_stats(ctx_, &s), "ykgpu_get_stats");
+    if (group_)
+      check(ykgpu_group_get_stats(group_, -1, &s), "ykgpu_group_get_stats");
+    else
+      check(ykgpu_get_stats(ctx_, &s), "ykgpu_get_stats");
     return s;
   }
 
  private:
+  // a group traces on a context of its first device, created on first use with the scene
+  void trace_context() {
+    if (!ctx_) check(ykgpu_context_create(devices_[0], &ctx_), "ykgpu_context_create");
+    if (!ctx_scene_) {
+      check(ykgpu_set_scene(ctx_, spheres_.data(), (uint32_t)spheres_.size(), &cam_), "ykgpu_set_scene");
+      ctx_scene_ = true;
+    }
+  }
+
+  std::vector<int> devices_;
   ykgpu_context* ctx_ = nullptr;
+  ykgpu_group* group_ = nullptr;
+  std::vector<yk_sphere> spheres_;
+  yk_camera cam_{};
+  bool ctx_scene_ = false;
 };
 
 }  // namespace ykgpu

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 7u
+#define YKGPU_ABI_VERSION 8u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 (reflected + fuzz * the reference's random_in_unit_sphere,
@@ -177,6 +177,9 @@ typedef struct yk_render_stats {
                               [0] leaf tests with disc >= 0 (root bounds computed), hits
                               shaded as [1] lambertian, [2] metal, [3] of them fuzzy,
                               [4] dielectric; [5..7] 0                                   */
+  uint64_t device_bytes;   /* device memory the context holds after the call: scene, BVHs,
+                              processing order, warm-up and colour rings, running sums, MT
+                              and attenuation scratch, output buffers      */
 } yk_render_stats;
 
 typedef struct ykgpu_context ykgpu_context;
@@ -238,6 +241,43 @@ int ykgpu_math_div(ykgpu_context* ctx, const double* num3, const double* den, do
 
 /* Statistics of the last render on this context. */
 int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out);
+
+/* ---- several devices in one process (BASELINE config 4: the image row-tiled across the 8 GPUs
+ * of a node) -------------------------------------------------------------------------------
+ * The reference calls render() once from main (source.cpp:221) on one thread; a group lets that
+ * one call use k devices.  A group holds one context per entry of `devices` (an entry may repeat:
+ * {0, 0, 0} runs three contexts on device 0, which the tests use on one-GPU machines).  Rows of
+ * the params' row set are dealt cyclically — tile row t goes to entry t mod k, the same dealing
+ * as the torch.distributed bench (uecraytracing_amd/tiles.py) — every entry renders its tile with
+ * ykgpu_render_async on its own streams, so the devices run concurrently, and each tile is
+ * copied from its device straight into its rows of the caller's image (a strided 2-D copy: the
+ * caller's image is on the host, so no device-side gather is needed before it).  Every row is
+ * independent (source.cpp:154-158), so the image equals one device's byte for byte.
+ * Row sets in bands (row_band_log2 > 0) are not dealt: YK_ERR_UNSUPPORTED when k > 1.
+ * Not reentrant per group, like a context. */
+typedef struct ykgpu_group ykgpu_group;
+
+int ykgpu_group_create(const int* devices, uint32_t n_devices, ykgpu_group** out);
+int ykgpu_group_destroy(ykgpu_group* group);
+/* Number of entries (contexts) of the group. */
+int ykgpu_group_size(const ykgpu_group* group, uint32_t* n);
+/* ykgpu_set_scene on every entry (each device holds the scene and its BVHs in its own HBM). */
+int ykgpu_group_set_scene(ykgpu_group* group, const yk_sphere* spheres, uint32_t count,
+                          const yk_camera* camera);
+/* The render loop over every entry; synchronous; rgb_host as for ykgpu_render
+ * (row_count * W * 3 bytes, the rows of params in order). */
+int ykgpu_group_render(ykgpu_group* group, const yk_render_params* params, uint8_t* rgb_host);
+/* Statistics of the last group render: index < n the entry's own (its tile), index -1 the whole
+ * call: samples and work counters summed over the entries, launches summed, kernel_ms /
+ * render_busy_ms / warmup_ms / resolve_ms the largest entry's, total_ms the call's host wall
+ * clock (copies included). */
+int ykgpu_group_get_stats(ykgpu_group* group, int index, yk_render_stats* out);
+
+/* One call for the whole drop-in: a group over `devices`, the scene, the render, the group
+ * released (scene upload and BVH builds are inside the call). */
+int ykgpu_render_devices(const int* devices, uint32_t n_devices, const yk_sphere* spheres,
+                         uint32_t count, const yk_camera* camera, const yk_render_params* params,
+                         uint8_t* rgb_host);
 
 /* ---- host-side scene helpers (no device needed) ---------------------------------------- */
 

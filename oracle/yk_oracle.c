@@ -226,9 +226,12 @@ static void* worker(void* arg) {
   job_t* j = (job_t*)arg;
   world_t w = {j->s, j->n, j->cam, j->p, 0, j->as_shipped};
   const uint32_t W = j->p->image_width;
-  for (uint32_t i = j->tid; i < j->p->row_count; i += j->nthreads) {
-    uint32_t y = row_y(j->p, i);
-    for (uint32_t x = 0; x < W; ++x) {
+  /* pixels dealt to the threads one by one (a single row still uses every thread) */
+  const uint64_t npix = (uint64_t)j->p->row_count * W;
+  for (uint64_t k = j->tid; k < npix; k += j->nthreads) {
+    const uint32_t i = (uint32_t)(k / W), x = (uint32_t)(k % W);
+    const uint32_t y = (uint32_t)row_y(j->p, i);
+    {
       c3 ps = pixel_sum(&w, y, x, &j->segs);
       size_t o = ((size_t)i * W + x) * 3;
       if (j->sums) { j->sums[o] = ps.r; j->sums[o + 1] = ps.g; j->sums[o + 2] = ps.b; }
@@ -258,7 +261,7 @@ static int check(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_
 /* ------------------------------------------------------------------ exported (ctypes) */
 
 /* Render the rows named by p into rgb (row_count*W*3 bytes) and/or sums (row_count*W*3
- * doubles), with `nthreads` host threads over interleaved rows.  Returns YK_* status;
+ * doubles), with `nthreads` host threads over interleaved pixels.  Returns YK_* status;
  * *segments / *tests (nullable) receive work counts. */
 static int render_impl(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p,
                        uint8_t* rgb, double* sums, int nthreads, uint64_t* segments, uint64_t* tests,

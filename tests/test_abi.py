@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = yk.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.ykgpu_abi_version() == 7
+    assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 8
 
 
 def test_reference_camera_matches_camera_hpp():
@@ -76,6 +76,36 @@ def test_no_cpu_fallback_without_a_gpu():
         pytest.skip("a GPU is visible")
     with pytest.raises(yk.YkError):
         yk.Renderer(0)
+
+
+def test_group_without_a_gpu_fails_loudly():
+    if yk.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(yk.YkError, match="group entry 0"):
+        yk.Group([0, 0])
+    arr, cam = yk.build_scene("ref4")
+    with pytest.raises(yk.YkError):
+        yk.render_devices([0], arr, cam, records.make_params(16, 9, 2))
+
+
+def test_group_invalid_arguments_are_reported():
+    lib = yk.load_library()
+    g = ctypes.c_void_p()
+    assert lib.ykgpu_group_create(None, 0, ctypes.byref(g)) == 1
+    assert b"empty device list" in lib.ykgpu_last_error()
+    devs = (ctypes.c_int * 1)(0)
+    assert lib.ykgpu_group_create(devs, 1, None) == 1
+    assert lib.ykgpu_group_render(None, None, None) == 1
+    assert lib.ykgpu_group_set_scene(None, None, 0, None) == 1
+    assert lib.ykgpu_group_get_stats(None, -1, None) == 1
+    n = ctypes.c_uint32(0)
+    assert lib.ykgpu_group_size(None, ctypes.byref(n)) == 1
+
+
+def test_render_stats_layout_matches_the_header():
+    """yk_render_stats ends with device_bytes at offset 312 (include/ykgpu.h, ABI 8)."""
+    assert records.RenderStats.device_bytes.offset == 312
+    assert ctypes.sizeof(records.RenderStats) == 320
 
 
 def test_invalid_arguments_are_reported():

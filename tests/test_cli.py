@@ -176,6 +176,44 @@ def test_patched_reference_200x112x8_and_default_size(tmp_path):
 
 
 @pytest.mark.gpu
+def test_patched_reference_on_several_devices(tmp_path):
+    """The patched source.cpp with YKGPU_DEVICES naming three contexts (the bridge's group: rows
+    dealt over them, include/ykgpu.h): the same PNG file as one device, at 200x112x8 (the golden)
+    and at 16x9x2 (the constexpr build's file), and -l 3 traces still equal the single device's."""
+    need(PATCHED["_200x8"])
+    need(PATCHED["_16x2"])
+    env = dict(os.environ, YKGPU_DEVICES="0,0,0")
+    for exe in (PATCHED["_200x8"], PATCHED["_16x2"]):
+        a, b = tmp_path / ("a" + os.path.basename(exe)), tmp_path / ("b" + os.path.basename(exe))
+        a.mkdir()
+        b.mkdir()
+        r = subprocess.run([exe, "image.png"], cwd=a, capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr
+        r2 = subprocess.run([exe, "image.png"], cwd=b, capture_output=True, text=True, timeout=300)
+        assert r2.returncode == 0, r2.stderr
+        assert (a / "image.png").read_bytes() == (b / "image.png").read_bytes()
+    rgb, W, H = golden_data.png_rgb(str(tmp_path / "araytrace_ykgpu_200x8" / "image.png"))
+    e = next(c for c in MAN["cases"] if c["name"] == "ref4_200x112x8_d50_s404")
+    assert golden_data.sha(np.frombuffer(rgb, np.uint8)) == e["rgb_sha256"]
+    a = subprocess.run([PATCHED["_16x2"], "-l", "3", "o.png"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=300, env=env)
+    b = subprocess.run([PATCHED["_16x2"], "-l", "3", "o.png"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=300)
+    assert a.returncode == b.returncode == 0 and a.stdout == b.stdout
+
+
+def test_patched_reference_rejects_a_bad_device_list(tmp_path):
+    """YKGPU_DEVICES that is not a device list fails loudly before any device is touched."""
+    need(PATCHED["_16x2"])
+    for bad in ("x", "0,,1", "-1", "0;1"):
+        r = subprocess.run([PATCHED["_16x2"], "o.png"], cwd=tmp_path, capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, YKGPU_DEVICES=bad))
+        assert r.returncode != 0
+        assert "YKGPU_DEVICES" in r.stderr, r.stderr
+        assert not (tmp_path / "o.png").exists()
+
+
+@pytest.mark.gpu
 def test_patched_reference_console_matches_runtime_build(tmp_path):
     """-v / -l 2: the unmodified runtime build's lines do not depend on its random seeds, so the
     patched build's whole stdout must equal it (cxxopts parsing, messages, setw widths)."""

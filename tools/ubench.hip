@@ -1,7 +1,9 @@
 // tools/ubench.hip — issue cost of single VALU instructions / short sequences on gfx950: one
 // wave per SIMD, eight independent chains, clock64() around the loop.  Diagnostic only: says
 // which FP64 / integer operations the render loop should avoid.
-//   build: hipcc -O3 --offload-arch=gfx950 -o tools/ubench tools/ubench.hip ; run: tools/ubench
+//   build: hipcc -O3 --offload-arch=gfx950 -o tools/ubench tools/ubench.hip ; run: tools/ubench [out.jsonl]
+// The JSON lines are the evidence of the roofline's FP64 VALU peak (profiles/r03_ubench.jsonl,
+// tools/valu_peak.py, bench.py).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -120,42 +122,118 @@ struct SqrtLibF64 {
 };
 
 template <class Op>
-__global__ __launch_bounds__(64) void bench(uint64_t* cyc, typename Op::T* sink, typename Op::T a,
+__global__ __launch_bounds__(64) void bench(uint64_t* cyc, uint64_t* rt, typename Op::T* sink, typename Op::T a,
                                             typename Op::T b, typename Op::T init) {
   using T = typename Op::T;
   T x[kChains];
 #pragma unroll
   for (int k = 0; k < kChains; ++k) x[k] = init;
+  const uint64_t r0 = wall_clock64();
   const uint64_t t0 = clock64();
   for (int i = 0; i < kIters; ++i) {
 #pragma unroll
     for (int k = 0; k < kChains; ++k) Op::op(x[k], a, b);
   }
   const uint64_t t1 = clock64();
+  const uint64_t r1 = wall_clock64();
   T s = x[0];
 #pragma unroll
   for (int k = 1; k < kChains; ++k) s = s + x[k];
   sink[blockIdx.x * 64 + threadIdx.x] = s;
-  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0, rt[blockIdx.x] = r1 - r0;
+}
+
+// JSON lines of the run (one per op and occupancy) for profiles/: ticks = shader clock cycles
+// (s_memtime); waves_per_simd = waves / (4 x CUs); simd_cycles_per_instr = ticks per op per wave
+// / waves_per_simd (the SIMD's issue cost of one wave64 instruction once it is saturated);
+// clock_mhz = ticks / s_memrealtime ticks x 100 MHz (the clock the chip held under this loop)
+static FILE* g_json = nullptr;
+static int g_cus = 0;
+
+// Chip-level throughput of one op: every SIMD holds `wps` waves of the same stream, the whole
+// launch timed with HIP events: lane-flops / elapsed.  The peak the roofline divides by is the
+// best of these for v_fma_f64 (tools/valu_peak.py).
+template <class Op>
+__global__ __launch_bounds__(64) void chip(typename Op::T* sink, typename Op::T a, typename Op::T b,
+                                           typename Op::T init, int iters) {
+  using T = typename Op::T;
+  T x[kChains];
+#pragma unroll
+  for (int k = 0; k < kChains; ++k) x[k] = init;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < kChains; ++k) Op::op(x[k], a, b);
+  }
+  T s = x[0];
+#pragma unroll
+  for (int k = 1; k < kChains; ++k) s = s + x[k];
+  sink[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
+template <class Op>
+void chip_rate(const char* name, double flops_per_lane_op, typename Op::T a, typename Op::T b,
+               typename Op::T init, int wps) {
+  using T = typename Op::T;
+  const int waves = wps * 4 * g_cus, iters = 16384;
+  T* sink;
+  (void)hipMalloc(&sink, (size_t)waves * 64 * sizeof(T));
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  float best = 1e30f;
+  for (int rep = 0; rep < 4; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    hipLaunchKernelGGL(chip<Op>, dim3(waves), dim3(64), 0, 0, sink, a, b, init, iters);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (rep > 0 && ms < best) best = ms;  // the first launch warms the clock
+  }
+  const double ops = (double)waves * iters * kChains;  // wave-instructions
+  const double tf = ops * 64 * flops_per_lane_op / (best * 1e-3) / 1e12;
+  const double cyc = (best * 1e-3) * 2.4e9 * 4 * g_cus / ops;  // SIMD cycles per wave-instr at 2.4 GHz
+  printf("chip %-12s waves/SIMD=%d  %.3f ms  %.2f TFLOP/s  (%.2f SIMD cycles per wave-instruction at 2.4 GHz)\n",
+         name, wps, best, tf, cyc);
+  if (g_json)
+    fprintf(g_json,
+            "{\"chip_op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"wave_instructions\": %.0f, "
+            "\"flops_per_lane_op\": %.0f, \"tflops\": %.3f, \"simd_cycles_per_instr_at_2400mhz\": %.4f}\n",
+            name, wps, best, ops, flops_per_lane_op, tf, cyc);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(sink);
 }
 
 template <class Op>
 void run(const char* name, typename Op::T a, typename Op::T b, typename Op::T init, int waves) {
   using T = typename Op::T;
-  uint64_t* cyc;
+  uint64_t *cyc, *rt;
   T* sink;
   (void)hipMalloc(&cyc, waves * sizeof(uint64_t));
+  (void)hipMalloc(&rt, waves * sizeof(uint64_t));
   (void)hipMalloc(&sink, waves * 64 * sizeof(T));
-  hipLaunchKernelGGL(bench<Op>, dim3(waves), dim3(64), 0, 0, cyc, sink, a, b, init);
-  hipLaunchKernelGGL(bench<Op>, dim3(waves), dim3(64), 0, 0, cyc, sink, a, b, init);
+  hipLaunchKernelGGL(bench<Op>, dim3(waves), dim3(64), 0, 0, cyc, rt, sink, a, b, init);
+  hipLaunchKernelGGL(bench<Op>, dim3(waves), dim3(64), 0, 0, cyc, rt, sink, a, b, init);
   (void)hipDeviceSynchronize();
-  uint64_t h[4096];
+  static uint64_t h[8192], hr[8192];
   (void)hipMemcpy(h, cyc, waves * sizeof(uint64_t), hipMemcpyDeviceToHost);
-  double mean = 0;
-  for (int i = 0; i < waves; ++i) mean += (double)h[i];
+  (void)hipMemcpy(hr, rt, waves * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  double mean = 0, mrt = 0;
+  for (int i = 0; i < waves; ++i) mean += (double)h[i], mrt += (double)hr[i];
   mean /= waves;
-  printf("%-12s waves=%5d  %.2f clock64 ticks per op per wave\n", name, waves, mean / ((double)kIters * kChains));
+  mrt /= waves;
+  const double per_wave = mean / ((double)kIters * kChains);
+  const double wps = (double)waves / (4.0 * g_cus);
+  printf("%-12s waves=%5d  %.2f clock64 ticks per op per wave  (%.2f SIMD cycles per wave-instruction, clock %.0f MHz)\n",
+         name, waves, per_wave, per_wave / wps, mean / mrt * 100.0);
+  if (g_json)
+    fprintf(g_json,
+            "{\"op\": \"%s\", \"waves\": %d, \"waves_per_simd\": %.3f, \"ticks_per_op_per_wave\": %.4f, "
+            "\"simd_cycles_per_instr\": %.4f, \"clock_mhz\": %.1f}\n",
+            name, waves, wps, per_wave, per_wave / wps, mean / mrt * 100.0);
   (void)hipFree(cyc);
+  (void)hipFree(rt);
   (void)hipFree(sink);
 }
 
@@ -203,12 +281,22 @@ void accuracy() {
          worst[1] * 0x1p52L, worst[2] * 0x1p52L);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1]: optional path of the JSON-lines summary
+  if (argc > 1) g_json = fopen(argv[1], "w");
   accuracy();
   hipDeviceProp_t p;
   (void)hipGetDeviceProperties(&p, 0);
+  g_cus = p.multiProcessorCount;
   printf("%s  CUs %d  clock %d kHz\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
-  for (int waves : {p.multiProcessorCount * 4, p.multiProcessorCount * 8}) {
+  if (g_json) fprintf(g_json, "{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d}\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
+  for (int wps : {1, 2, 4, 8}) {
+    chip_rate<FmaF32>("fma_f32", 2, 1.0000001f, 0.5f, 1.0f, wps);
+    chip_rate<PkFmaF32>("pk_fma_f32", 4, 1.0, 0.5, 1.0, wps);
+    chip_rate<FmaF64>("fma_f64", 2, 1.0000001, 0.5, 1.0, wps);
+    chip_rate<MulLoU32>("mul_lo_u32", 0, 1812433253u, 0, 7u, wps);
+  }
+  for (int waves : {p.multiProcessorCount * 4, p.multiProcessorCount * 8, p.multiProcessorCount * 16}) {
     run<FmaF32>("fma_f32", 1.0000001f, 0.5f, 1.0f, waves);
     run<PkFmaF32>("pk_fma_f32", 1.0, 0.5, 1.0, waves);
     run<MinMax3F32>("max3_f32", 1.0f, 0.5f, 1.0f, waves);
@@ -233,5 +321,6 @@ int main() {
     run<BfeU32>("bfe_u32", 0, 0, 0x3ff00000u, waves);
     run<XorShrU32>("xor_shr_u32", 0, 0, 7u, waves);
   }
+  if (g_json) fclose(g_json);
   return 0;
 }

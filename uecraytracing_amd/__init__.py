@@ -28,7 +28,10 @@ EXPORTS = (
     "ykgpu_context_destroy", "ykgpu_set_scene", "ykgpu_render", "ykgpu_render_async",
     "ykgpu_render_sums", "ykgpu_render_trace", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_sqrt_f32", "ykgpu_math_div", "yk_camera_reference", "yk_camera_look",
     "yk_scene_build", "yk_scene_write", "yk_scene_read", "yk_image_height_for",
+    "ykgpu_group_create", "ykgpu_group_destroy", "ykgpu_group_size", "ykgpu_group_set_scene",
+    "ykgpu_group_render", "ykgpu_group_get_stats", "ykgpu_render_devices",
 )
+ABI_VERSION = 8
 SCENE_DIR = os.path.join(PKG_DIR, "scenes")  # committed scene files of the BASELINE configs
 
 _lib = None
@@ -79,11 +82,19 @@ def load_library():
         "yk_scene_write": ([c.c_char_p, P(Sphere), c.c_uint32, P(Camera)], c.c_int),
         "yk_scene_read": ([c.c_char_p, P(Sphere), c.c_uint32, P(c.c_uint32), P(Camera)], c.c_int),
         "yk_image_height_for": ([c.c_uint32], c.c_uint32),
+        "ykgpu_group_create": ([P(c.c_int), c.c_uint32, P(c.c_void_p)], c.c_int),
+        "ykgpu_group_destroy": ([c.c_void_p], c.c_int),
+        "ykgpu_group_size": ([c.c_void_p, P(c.c_uint32)], c.c_int),
+        "ykgpu_group_set_scene": ([c.c_void_p, P(Sphere), c.c_uint32, P(Camera)], c.c_int),
+        "ykgpu_group_render": ([c.c_void_p, P(RenderParams), c.c_void_p], c.c_int),
+        "ykgpu_group_get_stats": ([c.c_void_p, c.c_int, P(RenderStats)], c.c_int),
+        "ykgpu_render_devices": ([P(c.c_int), c.c_uint32, P(Sphere), c.c_uint32, P(Camera),
+                                  P(RenderParams), c.c_void_p], c.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
         f.argtypes, f.restype = args, res
-    if lib.ykgpu_abi_version() != 7:
+    if lib.ykgpu_abi_version() != ABI_VERSION:
         raise YkError("ABI version mismatch")
     _lib = lib
     return lib
@@ -219,5 +230,64 @@ class Renderer:
         return st.as_dict()
 
 
-__all__ = ["Renderer", "YkError", "build_scene", "write_scene", "read_scene", "SCENE_DIR", "reference_camera", "device_count",
+class Group:
+    """Several device contexts in one process (ykgpu_group): rows dealt cyclically over the
+    entries, every tile copied into its rows of one host image (include/ykgpu.h)."""
+
+    def __init__(self, devices):
+        self._lib = load_library()
+        self._g = ctypes.c_void_p()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        _check(self._lib.ykgpu_group_create(devs, len(devices), ctypes.byref(self._g)))
+        self.devices = list(devices)
+
+    def close(self):
+        if self._g:
+            self._lib.ykgpu_group_destroy(self._g)
+            self._g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def size(self) -> int:
+        n = ctypes.c_uint32(0)
+        _check(self._lib.ykgpu_group_size(self._g, ctypes.byref(n)))
+        return n.value
+
+    def set_scene(self, spheres, camera: Camera):
+        arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
+        _check(self._lib.ykgpu_group_set_scene(self._g, arr, len(arr), ctypes.byref(camera)))
+
+    def render(self, params: RenderParams) -> np.ndarray:
+        out = np.empty((params.row_count, params.image_width, 3), np.uint8)
+        _check(self._lib.ykgpu_group_render(self._g, ctypes.byref(params), out.ctypes.data))
+        return out
+
+    def stats(self, index: int = -1) -> dict:
+        st = RenderStats()
+        _check(self._lib.ykgpu_group_get_stats(self._g, index, ctypes.byref(st)))
+        return st.as_dict()
+
+
+def render_devices(devices, spheres, camera: Camera, params: RenderParams) -> np.ndarray:
+    """ykgpu_render_devices: group, scene, render and release in one call."""
+    lib = load_library()
+    arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    out = np.empty((params.row_count, params.image_width, 3), np.uint8)
+    _check(lib.ykgpu_render_devices(devs, len(devices), arr, len(arr), ctypes.byref(camera),
+                                    ctypes.byref(params), out.ctypes.data))
+    return out
+
+
+__all__ = ["Renderer", "Group", "render_devices", "YkError", "build_scene", "write_scene", "read_scene", "SCENE_DIR", "reference_camera", "device_count",
            "make_params", "load_library", "records", "EXPORTS", "LIB_PATH", "CLI_PATH"]

@@ -1607,6 +1607,7 @@ struct DevTree {
   uint32_t depth = 0, n_nodes = 0;
   double origin_bound = 0;  // |o|_inf beyond which a ray takes the linear scan (< 0: every ray)
   uint32_t geo_off = 0, ids_off = 0;  // leaf geometry and ids in LDS, after the nodes
+  size_t bytes = 0;                   // device bytes of nodes, leaf geometry and ids
   // LDS plan per workgroup size: [0] kBlock (mt19937 instances), [1] kBlockX128 (xor128)
   struct Plan {
     bool in_lds = false;
@@ -1621,6 +1622,7 @@ struct DevTree {
     nodes = nullptr;
     leaf_geo = nullptr;
     leaf_ids = nullptr;
+    bytes = 0;
   }
 };
 
@@ -1669,6 +1671,14 @@ struct ykgpu_context {
   std::chrono::steady_clock::time_point t0;
 };
 
+struct ykgpu_group {
+  std::vector<ykgpu_context*> ctx;  // one per entry of the device list
+  std::vector<uint8_t*> tile;       // each entry's RGB8 tile on its device
+  std::vector<size_t> tile_cap;
+  std::vector<yk_render_stats> st;  // the last render's, per entry
+  yk_render_stats total{};          // ... and of the whole call
+};
+
 namespace {
 
 uint64_t host_row_y(const yk_render_params* p, uint32_t t) {
@@ -1701,6 +1711,11 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
   if (p->seed_mode != YK_SEED_COUNTER && p->seed_mode != YK_SEED_RANDOM_DEVICE)
     return fail(YK_ERR_UNSUPPORTED, "seed mode");
   if (!(p->t_min >= 0)) return fail(YK_ERR_INVALID, "t_min must be >= 0");
+  // the one-lane diagnostic exists only in the FP64 counting instance: anywhere else it would be
+  // ignored and a profile reconciled against the one-lane model would read all-lane counters
+  if ((p->flags & YK_FLAG_ONE_LANE) &&
+      (!(p->flags & YK_FLAG_COUNT_WORK) || p->precision != YK_PRECISION_FP64))
+    return fail(YK_ERR_INVALID, "YK_FLAG_ONE_LANE needs YK_FLAG_COUNT_WORK and FP64");
   return YK_OK;
 }
 
@@ -1731,6 +1746,9 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, size_t lanes, bool ne
 #define YK_COLOUR_MB 8192
 #endif
 constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colours per launch at most
+// a launch's slots are bounded by the colour budget (kmax in launch()), and the render kernel
+// addresses a slot's StartRec as 3 * slot uint4s in 32-bit arithmetic
+static_assert(kColourBytes / (8 * kColStride) * 3 < (1ull << 32), "3 * slot must fit 32 bits");
 // samples per pixel per launch at most: many mid-sized launches beat a few big ones, because the
 // launches alternate between two streams and each one's drain overlaps the next one's start
 // (round 1, 1920x1080x512 259.5 -> 254.0 ms at 64 spp/launch; with the render
@@ -2088,6 +2106,19 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   return YK_OK;
 }
 
+// Device memory the context holds (yk_render_stats.device_bytes)
+uint64_t device_bytes(const ykgpu_context* ctx) {
+  uint64_t b = ctx->t64.bytes + ctx->t32.bytes;
+  if (ctx->d_geo) b += (uint64_t)ctx->nspheres * (sizeof(SphereGeo) + sizeof(SphereMat) + sizeof(float4));
+  b += ctx->warm_cap + ctx->col_cap * sizeof(double) + ctx->acc_cap * sizeof(double);
+  b += (uint64_t)ctx->order_slots * sizeof(uint32_t) + (uint64_t)ctx->counter_cap * sizeof(uint32_t);
+  b += kCounters * sizeof(unsigned long long);
+  if (ctx->d_mt) b += 2ull * ctx->scratch_lanes * ykd::kMtN * sizeof(uint32_t);
+  if (ctx->d_ids) b += 2ull * ctx->id_lanes * ctx->id_stride * sizeof(uint16_t);
+  b += ctx->rgb_cap + ctx->sums_cap * sizeof(double);
+  return b;
+}
+
 int finish_stats(ykgpu_context* ctx) {
   if (!ctx->stats_pending) return YK_OK;
   YK_HIP(hipEventSynchronize(ctx->ev1));
@@ -2134,6 +2165,7 @@ int finish_stats(ykgpu_context* ctx) {
   ctx->stats.sphere_tests = c[1];
   ctx->stats.sqrt_calls = c[2];
   ctx->stats.mt_fallbacks = c[3];
+  ctx->stats.device_bytes = device_bytes(ctx);
   ctx->stats_pending = false;
   return YK_OK;
 }
@@ -2168,6 +2200,7 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
     YK_HIP(hipMemcpy(t.nodes, snodes.data(), snodes.size() * sizeof(DevNode), hipMemcpyHostToDevice));
   YK_HIP(hipMemcpy(t.leaf_geo, leaf_geo.data(), count * elem, hipMemcpyHostToDevice));
   YK_HIP(hipMemcpy(t.leaf_ids, bvh.order.data(), count * sizeof(uint32_t), hipMemcpyHostToDevice));
+  t.bytes = nn * sizeof(DevNode) + count * elem + count * sizeof(uint32_t);
   t.root = root_code;
   t.depth = bvh.depth;
   t.origin_bound = bvh.origin_bound;
@@ -2324,8 +2357,11 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   }
   YK_HIP(hipSetDevice(ctx->device));
   // a render enqueued by ykgpu_render_async on the caller's stream (and its launches on the
-  // context's own streams) may still read the scene: wait for the whole device
-  YK_HIP(hipDeviceSynchronize());
+  // context's own streams) may still read the scene: wait for this context's last call — ev1
+  // follows the call's final reduce, which follows every launch of the call (launch()) — and for
+  // its own stream (the diagnostic entry points), not for the rest of the device
+  YK_HIP(hipEventSynchronize(ctx->ev1));
+  YK_HIP(hipStreamSynchronize(ctx->stream));
   if (count > ctx->nspheres || !ctx->d_geo) {
     (void)hipFree(ctx->d_geo);
     (void)hipFree(ctx->d_mat);
@@ -2534,6 +2570,164 @@ int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out) {
   if (rc) return rc;
   *out = ctx->stats;
   return YK_OK;
+}
+
+// ---- several devices in one process (include/ykgpu.h "several devices") ----------------------
+// One context per entry; rows dealt cyclically over the entries (tile row t of the call's row set
+// → entry t mod k, uecraytracing_amd/tiles.py's dealing); every entry renders its tile into a
+// device buffer on its own streams, and the tile is copied from its device straight into its rows
+// of the caller's host image by one strided 2-D copy: the image ends on the host anyway (stb
+// writes it), so a device-side gather first would only add a hop.
+int ykgpu_group_create(const int* devices, uint32_t n_devices, ykgpu_group** out) {
+  if (!out) return fail(YK_ERR_INVALID, "null out");
+  *out = nullptr;
+  if (!devices || n_devices == 0) return fail(YK_ERR_INVALID, "empty device list");
+  if (n_devices > 64) return fail(YK_ERR_INVALID, "at most 64 entries per group");
+  auto* g = new ykgpu_group();
+  for (uint32_t k = 0; k < n_devices; ++k) {
+    ykgpu_context* c = nullptr;
+    const int rc = ykgpu_context_create(devices[k], &c);
+    if (rc) {
+      const std::string msg = g_last_error;
+      ykgpu_group_destroy(g);
+      return fail(rc, "group entry " + std::to_string(k) + " (device " + std::to_string(devices[k]) + "): " + msg);
+    }
+    g->ctx.push_back(c);
+  }
+  g->tile.assign(n_devices, nullptr);
+  g->tile_cap.assign(n_devices, 0);
+  g->st.assign(n_devices, yk_render_stats{});
+  *out = g;
+  return YK_OK;
+}
+
+int ykgpu_group_destroy(ykgpu_group* g) {
+  if (!g) return YK_OK;
+  for (size_t k = 0; k < g->ctx.size(); ++k) {
+    if (k < g->tile.size() && g->tile[k]) {
+      (void)hipSetDevice(g->ctx[k]->device);
+      (void)hipStreamSynchronize(g->ctx[k]->stream);
+      (void)hipFree(g->tile[k]);
+    }
+    ykgpu_context_destroy(g->ctx[k]);
+  }
+  delete g;
+  return YK_OK;
+}
+
+int ykgpu_group_size(const ykgpu_group* g, uint32_t* n) {
+  if (!g || !n) return fail(YK_ERR_INVALID, "null argument");
+  *n = (uint32_t)g->ctx.size();
+  return YK_OK;
+}
+
+int ykgpu_group_set_scene(ykgpu_group* g, const yk_sphere* spheres, uint32_t count, const yk_camera* camera) {
+  if (!g) return fail(YK_ERR_INVALID, "null group");
+  for (ykgpu_context* c : g->ctx) {
+    const int rc = ykgpu_set_scene(c, spheres, count, camera);
+    if (rc) return rc;
+  }
+  return YK_OK;
+}
+
+int ykgpu_group_render(ykgpu_group* g, const yk_render_params* p, uint8_t* rgb_host) {
+  if (!g || !p || !rgb_host) return fail(YK_ERR_INVALID, "null argument");
+  const uint32_t k = (uint32_t)g->ctx.size();
+  int rc = check_params(g->ctx[0], p);
+  if (rc) return rc;
+  if (k > 1 && p->row_band_log2 != 0)
+    return fail(YK_ERR_UNSUPPORTED, "a group deals single rows: row_band_log2 must be 0");
+  if (k > 1 && (uint64_t)p->row_stride * k >= (1ull << 32)) return fail(YK_ERR_INVALID, "row_stride * devices overflows");
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t row_bytes = (size_t)p->image_width * 3;
+  std::vector<yk_render_params> sub(k, *p);
+  std::vector<uint32_t> rows(k, 0);
+  // 1. every entry's tile enqueued on its own device before any copy: the devices run together
+  for (uint32_t e = 0; e < k; ++e) {
+    rows[e] = p->row_count > e ? (p->row_count - e + k - 1) / k : 0;
+    if (!rows[e]) continue;
+    sub[e].row_begin = p->row_begin + e * p->row_stride;
+    sub[e].row_stride = p->row_stride * k;
+    sub[e].row_count = rows[e];
+    ykgpu_context* c = g->ctx[e];
+    YK_HIP(hipSetDevice(c->device));
+    const size_t need = rows[e] * row_bytes;
+    if (need > g->tile_cap[e]) {
+      (void)hipStreamSynchronize(c->stream);
+      (void)hipFree(g->tile[e]);
+      g->tile[e] = nullptr;
+      g->tile_cap[e] = 0;
+      YK_HIP(hipMalloc(&g->tile[e], need));
+      g->tile_cap[e] = need;
+    }
+    if ((rc = ykgpu_render_async(c, &sub[e], g->tile[e], nullptr))) return rc;
+  }
+  // 2. each tile into rows e, e + k, e + 2k, ... of the caller's image (ordered after its render
+  //    on the entry's stream)
+  for (uint32_t e = 0; e < k; ++e) {
+    if (!rows[e]) continue;
+    ykgpu_context* c = g->ctx[e];
+    YK_HIP(hipSetDevice(c->device));
+    YK_HIP(hipMemcpy2DAsync(rgb_host + e * row_bytes, row_bytes * k, g->tile[e], row_bytes, row_bytes, rows[e],
+                            hipMemcpyDeviceToHost, c->stream));
+  }
+  yk_render_stats tot{};
+  for (uint32_t e = 0; e < k; ++e) {
+    g->st[e] = yk_render_stats{};
+    if (!rows[e]) continue;
+    ykgpu_context* c = g->ctx[e];
+    YK_HIP(hipSetDevice(c->device));
+    YK_HIP(hipStreamSynchronize(c->stream));
+    if ((rc = finish_stats(c))) return rc;
+    g->st[e] = c->stats;
+    const yk_render_stats& s = c->stats;
+    tot.samples += s.samples;
+    tot.segments += s.segments;
+    tot.sphere_tests += s.sphere_tests;
+    tot.sqrt_calls += s.sqrt_calls;
+    tot.mt_fallbacks += s.mt_fallbacks;
+    tot.node_visits += s.node_visits;
+    tot.linear_scans += s.linear_scans;
+    tot.newton_calls += s.newton_calls;
+    tot.newton_iters += s.newton_iters;
+    for (int q = 0; q < 8; ++q) tot.work[q] += s.work[q];
+    tot.launches += s.launches;
+    tot.grid_blocks = std::max(tot.grid_blocks, s.grid_blocks);
+    tot.kernel_ms = std::max(tot.kernel_ms, s.kernel_ms);
+    tot.render_busy_ms = std::max(tot.render_busy_ms, s.render_busy_ms);
+    tot.warmup_ms = std::max(tot.warmup_ms, s.warmup_ms);
+    tot.resolve_ms = std::max(tot.resolve_ms, s.resolve_ms);
+    tot.seed_key = s.seed_key;
+    tot.device_bytes += s.device_bytes + g->tile_cap[e];
+  }
+  tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  g->total = tot;
+  return YK_OK;
+}
+
+int ykgpu_group_get_stats(ykgpu_group* g, int index, yk_render_stats* out) {
+  if (!g || !out) return fail(YK_ERR_INVALID, "null argument");
+  if (index == -1) {
+    *out = g->total;
+    return YK_OK;
+  }
+  if (index < 0 || (size_t)index >= g->ctx.size()) return fail(YK_ERR_INVALID, "entry index out of range");
+  *out = g->st[index];
+  return YK_OK;
+}
+
+int ykgpu_render_devices(const int* devices, uint32_t n_devices, const yk_sphere* spheres, uint32_t count,
+                         const yk_camera* camera, const yk_render_params* p, uint8_t* rgb_host) {
+  ykgpu_group* g = nullptr;
+  int rc = ykgpu_group_create(devices, n_devices, &g);
+  if (!rc) rc = ykgpu_group_set_scene(g, spheres, count, camera);
+  if (!rc) rc = ykgpu_group_render(g, p, rgb_host);
+  if (g) {
+    const std::string msg = g_last_error;
+    ykgpu_group_destroy(g);
+    g_last_error = msg;
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -20,6 +20,45 @@ its lanes executed, which is what the implementation model predicts.
 """
 from __future__ import annotations
 
+import json
+import os
+
+# --- the roofline's peak ---------------------------------------------------------------------
+# The FP64 VALU peak is MEASURED, not the datasheet's: tools/ubench.hip times whole launches of
+# pure v_fma_f64 streams (8 independent chains per lane, 1-8 waves per SIMD on every SIMD of the
+# chip) with HIP events, and the best rate is the peak (profiles/<tag>_ubench.jsonl).  The
+# datasheet's MI355X FP64 vector figure is kept beside it for reference.
+SPEC_FP64_VALU_TFLOPS = 78.6
+UBENCH_EVIDENCE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                               "profiles", "r03_ubench.jsonl")
+
+
+def ubench_rows(path: str = UBENCH_EVIDENCE):
+    with open(path) as f:
+        return [json.loads(line) for line in f if line.strip()]
+
+
+def fp64_valu_peak(path: str = UBENCH_EVIDENCE):
+    """(peak TFLOP/s, evidence dict): the best chip-level v_fma_f64 rate in the ubench file."""
+    rows = ubench_rows(path)
+    fma = [r for r in rows if r.get("chip_op") == "fma_f64"]
+    if not fma:
+        raise ValueError(f"{path}: no chip-level fma_f64 rows")
+    best = max(fma, key=lambda r: r["tflops"])
+    f32 = [r for r in rows if r.get("chip_op") == "fma_f32"]
+    pk = [r for r in rows if r.get("chip_op") == "pk_fma_f32"]
+    ev = {
+        "source": os.path.relpath(path, os.path.dirname(os.path.dirname(path))),
+        "method": "tools/ubench.hip: whole launches of v_fma_f64 (8 independent chains per lane) on "
+                  "every SIMD, HIP-event timed, best of 1/2/4/8 waves per SIMD",
+        "fma_f64_tflops_by_waves_per_simd": {str(r["waves_per_simd"]): r["tflops"] for r in fma},
+        "fma_f64_simd_cycles_per_instr_at_2400mhz": best["simd_cycles_per_instr_at_2400mhz"],
+        "fma_f32_best_tflops": max((r["tflops"] for r in f32), default=None),
+        "pk_fma_f32_best_tflops": max((r["tflops"] for r in pk), default=None),
+        "spec_fp64_vector_tflops": SPEC_FP64_VALU_TFLOPS,
+    }
+    return best["tflops"], ev
+
 # --- algorithmic (reference expressions) -------------------------------------------------
 ALG_PER_SPHERE_TEST = 17  # sphere.hpp:29-33: oc (3), dot (5), len2 - r^2 (6), hb^2 - a*c (3)
 ALG_PER_ROOT = 4          # sphere.hpp:36-39: (-hb -/+ sq) / a, one or two roots

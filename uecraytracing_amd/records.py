@@ -112,6 +112,7 @@ class RenderStats(ctypes.Structure):
         ("grid_blocks", ctypes.c_uint32),
         ("render_busy_ms", ctypes.c_double),
         ("work", ctypes.c_uint64 * 8),
+        ("device_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -126,6 +127,7 @@ class RenderStats(ctypes.Structure):
 assert ctypes.sizeof(Sphere) == 80
 assert ctypes.sizeof(Camera) == 19 * 8
 assert ctypes.sizeof(RenderParams) == 72
+assert ctypes.sizeof(RenderStats) == 320
 
 
 def image_height_for(width: int) -> int:
