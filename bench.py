@@ -326,7 +326,8 @@ def main():
             "image": f"{W}x{H}", "spp": spp, "max_depth": depth, "spheres": len(spheres),
             "scene_file": os.path.relpath(scene_file, ROOT) if scene_file else None,
             "partition": f"rows dealt cyclically in bands of {1 << BAND_LOG2} over {world} GPU(s), "
-                         f"RCCL gather to rank 0",
+                         + ("RCCL gather to rank 0" if backend == "nccl" else
+                            f"{backend} gather to rank 0 through the host (rehearsal: ranks share a GPU)"),
         },
         "scene_upload_ms": round(scene_upload_ms, 3),
         "value_incl_scene_upload": round(total_samples * args.steps

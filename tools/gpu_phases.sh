@@ -1,4 +1,4 @@
-# Phase split (YK_ABLATE=8 stamp builds) of lib/abl variants, on the GPU box.
+# Phase split (stamp builds: -DYK_STAMPS=1, `make -C uecraytracing_amd/csrc stamps` → lib/abl/libykgpu_stamps.so) of lib/abl variants, on the GPU box.
 # usage: bash tools/gpu_phases.sh <spp> <variant> ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT

@@ -196,6 +196,7 @@ int main(int argc, char** argv) {
   std::mt19937_64 rng(1);
   std::uniform_real_distribution<double> U(0, 1);
   std::vector<std::pair<V, V>> seg;
+  std::vector<int> seg_depth;
   const int W = 192, H = 108;
   for (int y = 0; y < H; ++y)
     for (int x = 0; x < W; ++x)
@@ -205,6 +206,7 @@ int main(int argc, char** argv) {
         V d = sub(add(add(ld(cam.lower_left_corner), mul(ld(cam.horizontal), u)), mul(ld(cam.vertical), v)), o);
         for (int depth = 0; depth < 50; ++depth) {
           seg.push_back({o, d});
+          seg_depth.push_back(depth);
           double t;
           int id = M.hit_exact(o, d, t);
           if (id < 0) break;
@@ -236,7 +238,32 @@ int main(int argc, char** argv) {
       }
   std::vector<size_t> idx(seg.size());
   for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+  // YKSIM_SECONDARY=1: the bounce segments only (what the render loop would run if the first
+  // segment of every sample were done elsewhere)
+  if (getenv("YKSIM_SECONDARY")) {
+    std::vector<size_t> keep;
+    for (size_t i : idx)
+      if (seg_depth[i] > 0) keep.push_back(i);
+    idx.swap(keep);
+  }
   std::shuffle(idx.begin(), idx.end(), rng);
+  // YKSIM_PRIMARY=1: only the camera rays, a wave = one 8x8 pixel block at one sample (the
+  // coherent first segment: how many wave-level iterations a batch of primary rays needs)
+  if (getenv("YKSIM_PRIMARY")) {
+    seg.clear();
+    idx.clear();
+    for (int by = 0; by < H; by += 8)
+      for (int bx = 0; bx < W; bx += 8)
+        for (int k = 0; k < 64; ++k) {
+          const int x = bx + k % 8, y = by + k / 8;
+          if (x >= W || y >= H) continue;
+          double u = (x + U(rng)) / W, v = (H - y - 1 + U(rng)) / H;
+          V o = ld(cam.origin);
+          V d = sub(add(add(ld(cam.lower_left_corner), mul(ld(cam.horizontal), u)), mul(ld(cam.vertical), v)), o);
+          idx.push_back(seg.size());
+          seg.push_back({o, d});
+        }
+  }
   auto rcp = [](float x) { return std::fabs(x) > 1e-30f ? 1.0f / x : std::copysign(1e30f, x); };
 
   printf("%s n=%u leaf<=%u wide nodes %zu depth %u | %zu segments | weights visit %.0f leaf %.0f disc %.0f trip %.0f\n",

@@ -1,4 +1,4 @@
-"""Per-phase wave-cycle shares from the YK_ABLATE=8 stamp build (diagnostic only)."""
+"""Per-phase wave-cycle shares from the stamp build (yk_stamps.hpp, -DYK_STAMPS=1; diagnostic only)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import uecraytracing_amd as yk

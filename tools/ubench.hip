@@ -61,6 +61,14 @@ struct MulLoU32 {
   using T = uint32_t;
   static __device__ void op(T& x, T a, T) { asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(x) : "v"(a)); }
 };
+struct MadU64U32 {  // the walk step's multiply-add (low word of t * c + i), addend from SGPRs
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T) {
+    uint64_t r, cc;
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 7" : "=v"(r), "=s"(cc) : "v"(x), "v"(a));
+    x = (uint32_t)r;
+  }
+};
 struct XorShrU32 {  // x ^ (x >> 30): the seeding step's shift-xor
   using T = uint32_t;
   static __device__ void op(T& x, T, T) {
@@ -295,6 +303,8 @@ int main(int argc, char** argv) {
     chip_rate<PkFmaF32>("pk_fma_f32", 4, 1.0, 0.5, 1.0, wps);
     chip_rate<FmaF64>("fma_f64", 2, 1.0000001, 0.5, 1.0, wps);
     chip_rate<MulLoU32>("mul_lo_u32", 0, 1812433253u, 0, 7u, wps);
+    chip_rate<MadU64U32>("mad_u64_u32", 0, 1812433253u, 0, 7u, wps);
+    chip_rate<XorShrU32>("xor_shr_u32", 0, 0, 0, 7u, wps);
   }
   for (int waves : {p.multiProcessorCount * 4, p.multiProcessorCount * 8, p.multiProcessorCount * 16}) {
     run<FmaF32>("fma_f32", 1.0000001f, 0.5f, 1.0f, waves);

@@ -174,28 +174,6 @@ Built build(const double* centers, const double* radii, uint32_t n, double camer
   return out;
 }
 
-static int32_t slab_code(int32_t c) { return c >= 0 ? c * (int32_t)sizeof(SlabNode) : c; }
-
-std::vector<SlabNode> slab_nodes(const Built& b) {
-  std::vector<SlabNode> out(b.nodes.size());
-  for (size_t i = 0; i < b.nodes.size(); ++i) {
-    const Node& n = b.nodes[i];
-    SlabNode& s = out[i];
-    const float* lo[3] = {n.lo_x, n.lo_y, n.lo_z};
-    const float* hi[3] = {n.hi_x, n.hi_y, n.hi_z};
-    float* ax[3] = {s.x, s.y, s.z};
-    for (int a = 0; a < 3; ++a) {
-      ax[a][0] = lo[a][0], ax[a][1] = lo[a][1];
-      ax[a][2] = hi[a][0], ax[a][3] = hi[a][1];
-      ax[a][4] = lo[a][0], ax[a][5] = lo[a][1];
-    }
-    s.child[0] = slab_code(n.child[0]);
-    s.child[1] = slab_code(n.child[1]);
-  }
-  return out;
-}
-
-int32_t slab_root(const Built& b) { return slab_code(b.root); }
 
 namespace {
 struct Slot {

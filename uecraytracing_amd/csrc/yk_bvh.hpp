@@ -26,25 +26,13 @@ struct alignas(16) Node {
 };
 static_assert(sizeof(Node) == 64, "Node layout");
 
-// Device layout of a Node (80 bytes), built by slab_nodes().  Per axis, both children's planes
-// as [lo pair][hi pair][lo pair]: a ray whose 1/d on that axis is >= 0 reads (near, far) =
-// (lo, hi) at byte 0 of the axis, a ray with 1/d < 0 reads (hi, lo) at byte 8 — one 16-byte
-// read per axis returns the planes already ordered, so the slab test needs no min/max
-// (rounding is monotonic, so the selection equals min/max of the two products).  child >= 0 is
-// the BYTE OFFSET of an inner node (no multiply per visit); leaves keep their negative codes.
-// (80 bytes matters: with the 485-sphere scene, nodes + geometry + stacks of a 256-thread block
-// fit 3 blocks per CU in 160 KB of LDS; an 88-byte node with a second child copy does not.)
-struct alignas(16) SlabNode {
-  float x[6], y[6], z[6];
-  int32_t child[2];
-};
-static_assert(sizeof(SlabNode) == 80, "SlabNode layout");
-
 // 4-wide device node (160 bytes), built by wide_nodes() by collapsing the binary tree: each slot
 // whose child is an inner node is replaced by that node's two children, the largest surface
 // area first, until the node has 4 slots or only leaves.  Per axis, the 4 slots' planes as
 // [lo x4][hi x4][lo x4]: a ray with 1/d >= 0 reads (near x4, far x4) at bytes (0, 16) of the
-// axis, a ray with 1/d < 0 at (16, 32) — the SlabNode trick with 16-byte reads.  child >= 0 is
+// axis, a ray with 1/d < 0 at (16, 32) — one 16-byte read per plane set returns the planes
+// already ordered, so the slab test needs no min/max (rounding is monotonic, so the selection
+// equals min/max of the two products).  child >= 0 is
 // the BYTE OFFSET of an inner WideNode, < 0 a leaf code; an unused slot has an empty box
 // (lo = +3e38, hi = -3e38: near > far for any ray) and the empty leaf code ~0 (no spheres).
 // The culling per slot is the binary node's (same planes, same rounding): DESIGN.md §4 holds.
@@ -89,9 +77,6 @@ struct Options {
 // centers: 3 doubles per sphere; radii may be negative (hollow shells: |r| is used).
 Built build(const double* centers, const double* radii, uint32_t n, double camera_extent,
             const Options& opt = Options());
-// Nodes in SlabNode layout, and the root code in that encoding (byte offset or leaf code).
-std::vector<SlabNode> slab_nodes(const Built& b);
-int32_t slab_root(const Built& b);
 // 4-wide nodes (DFS order, root first), the root code in that encoding, and the wide depth
 // (inner nodes on the longest root-to-leaf path).
 std::vector<WideNode> wide_nodes(const Built& b, int32_t* root_code, uint32_t* wide_depth);

@@ -35,17 +35,7 @@ __device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.
 // ulp) ends at the reference's value after 1-2 steps instead of 5-17.  Checked against the
 // reference loop on every s = 2^k +- m ulp (k = -1074..1023, m < 2e5: 8.4e8 values) and 3e7
 // random values: only the smallest subnormal differs (s/2 underflows to 0), hence the guard
-// below, under which the reference start is kept.  YK_NEWTON_REF_START=1 restores the
-// reference start everywhere (A/B timing).  The iteration bound only matters for NaN/inf.
-// YK_ABLATE (timing-only builds, tools/ablate.py; results are WRONG by design):
-//   1 = skip the MT warm-up walk, 2 = hardware sqrt instead of math::sqrt, (8: phase stamps,
-//   no change of results), 32 = no attenuation unwind, 64 = no colour stores
-#ifndef YK_ABLATE
-#define YK_ABLATE 0
-#endif
-#ifndef YK_NEWTON_REF_START
-#define YK_NEWTON_REF_START 0
-#endif
+// below, under which the reference start is kept.  The iteration bound only matters for NaN/inf.
 // ---- division and square roots without the special-case steps ------------------------------
 // A correctly rounded double division on gfx950 is the compiler's sequence
 //   div_scale(d), div_scale(n), rcp, 4 fma (reciprocal refinement), mul, fma (residual),
@@ -56,15 +46,6 @@ __device__ __forceinline__ double len2(v3 a) { return a.x * a.x + a.y * a.y + a.
 // arithmetic, operation for operation, minus those steps -- and the refined reciprocal depends
 // only on the divisor, so it is computed once for a vector / scalar.  Bit-identical to `/`:
 // checked by tests/test_gpu_parity.py::test_fast_division_is_ieee_division (ykgpu_math_div).
-#ifndef YK_DIVFAST
-#define YK_DIVFAST 1
-#endif
-#ifndef YK_BOUNDAPPROX
-#define YK_BOUNDAPPROX 1
-#endif
-#ifndef YK_NEWTONFAST
-#define YK_NEWTONFAST 1
-#endif
 __device__ __forceinline__ bool div_range(double x) { return fabs(x) >= 0x1p-400 && fabs(x) <= 0x1p400; }
 __device__ __forceinline__ bool num_range(double x) { return x == 0.0 || div_range(x); }
 __device__ __forceinline__ double rcp_refined(double s) {
@@ -91,7 +72,6 @@ __device__ __forceinline__ double div_pos(double n, double s, double r) {
 // the range, the whole wave recomputes with the full division (same bits for in-range lanes), so
 // there is no per-lane branch nest.
 __device__ __forceinline__ v3 divs_fast(v3 a, double s) {
-  if (!YK_DIVFAST) return divs(a, s);
   const double r = rcp_refined(s);
   v3 q = {div_by(a.x, s, r), div_by(a.y, s, r), div_by(a.z, s, r)};
   const bool ok = div_range(s) && num_range(a.x) && num_range(a.y) && num_range(a.z);
@@ -101,7 +81,6 @@ __device__ __forceinline__ v3 divs_fast(v3 a, double s) {
 // n / d for n >= 0 and a small integer d with y = RN(1/d) from the host: Markstein's theorem
 // (y correctly rounded, q0 = RN(n*y) within an ulp => fma(fma(-d, q0, n), y, q0) = RN(n/d)).
 __device__ __forceinline__ double div_markstein(double n, double d, double y) {
-  if (!YK_DIVFAST) return n / d;
   const double q0 = n * y;
   return __builtin_fma(__builtin_fma(-d, q0, n), y, q0);
 }
@@ -110,14 +89,12 @@ __device__ __forceinline__ double div_markstein(double n, double d, double y) {
 // v_rsq_f64 / v_rcp_f64 are within 2^-23 (ISA: 2^29 ulp; measured 2^-24.2), one Newton step
 // squares that: relative error < 2^-44.
 __device__ __forceinline__ double sqrt_bound(double x) {  // x >= 0
-  if (!YK_BOUNDAPPROX) return __builtin_sqrt(x);
   const double r = __builtin_amdgcn_rsq(x);
   const double y = x * r, h = 0.5 * r;
   const double y1 = __builtin_fma(__builtin_fma(-y, y, x), h, y);
   return x == 0.0 ? 0.0 : y1;
 }
 __device__ __forceinline__ double rcp_bound(double a) {  // a > 0
-  if (!YK_BOUNDAPPROX) return 1.0 / a;
   const double r0 = __builtin_amdgcn_rcp(a);
   return __builtin_fma(r0, __builtin_fma(-a, r0, 1.0), r0);
 }
@@ -137,8 +114,7 @@ __device__ __forceinline__ double sqrt_start(double s) {
 
 __device__ __forceinline__ double nsqrt_impl(double s, uint32_t& iters) {
   double x, prev = 0.0;
-#if !YK_NEWTON_REF_START
-  if (YK_NEWTONFAST && s >= 0x1p-400 && s <= 0x1p400) {
+  if (s >= 0x1p-400 && s <= 0x1p400) {
     // ONE step from r = RN(sqrt(s)) lands on the loop's fixed point: in ulps of r,
     // fl(s/r) = r + RN(2(sqrt(s) - r)), so g(r) is r or the neighbour that the sum's
     // round-to-even picks, and that neighbour is the fixed point.  Checked against the
@@ -150,9 +126,6 @@ __device__ __forceinline__ double nsqrt_impl(double s, uint32_t& iters) {
     return (x + div_pos(s, x, rcp_refined(x))) / 2.0;
   }
   x = (s >= 0x1p-1000 && s <= 0x1.fffffffffffffp+1023) ? __builtin_sqrt(s) : s / 2.0;
-#else
-  x = s / 2.0;
-#endif
   for (int guard = 0; x != prev && guard < 4096; ++guard) {
     prev = x;
     x = (x + s / x) / 2.0;
@@ -161,9 +134,6 @@ __device__ __forceinline__ double nsqrt_impl(double s, uint32_t& iters) {
   return x;
 }
 __device__ __forceinline__ double nsqrt(double s) {
-#if YK_ABLATE & 2
-  return sqrt(s);
-#endif
   uint32_t it = 0;
   return nsqrt_impl(s, it);
 }
@@ -171,9 +141,6 @@ __device__ __forceinline__ double nsqrt(double s) {
 // Same, counting calls and loop iterations (work counters of the roofline model).
 __device__ __forceinline__ double nsqrt_c(double s, uint32_t& calls, uint32_t& iters) {
   ++calls;
-#if YK_ABLATE & 2
-  return sqrt(s);
-#endif
   return nsqrt_impl(s, iters);
 }
 
@@ -230,12 +197,8 @@ __device__ __forceinline__ void mt_start(MtLane& g, uint32_t seed) {
   g.a0 = seed;
   uint32_t x = mt_seed_step(seed, 1);
   g.a1 = x;
-#if YK_ABLATE & 1
-  x ^= 0x5bd1e995u;
-#else
 #pragma unroll 8
   for (uint32_t i = 2; i <= kMtM; ++i) x = mt_seed_step(x, i);
-#endif
   g.b = x;
 }
 
@@ -248,13 +211,35 @@ __device__ __forceinline__ void mt_start_from(MtLane& g, uint32_t seed, uint32_t
   g.b = x397;
 }
 
+#ifndef YK_WALK_MAD
+#define YK_WALK_MAD 0
+#endif
+// One seeding step whose index is wave-uniform (the walk's loop counter, in SGPRs): the multiply
+// and the add of i as ONE v_mad_u64_u32 (low word of t * 1812433253 + i), three instructions
+// instead of four (xor-shift, v_mul_lo_u32, v_add).  cmul holds 1812433253 in a VGPR: the
+// instruction may read one SGPR operand, the 64-bit addend.
+__device__ __forceinline__ uint32_t mt_seed_step_mad(uint32_t prev, uint64_t i, uint32_t cmul) {
+  const uint32_t t = prev ^ (prev >> 30);
+  uint64_t r, carry;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(t), "v"(cmul), "s"(i));
+  return (uint32_t)r;
+}
+
 // x_397 of the seeding sequence (random.hpp:69-81) for N seeds at once (independent chains
-// interleaved for ILP).  Under YK_ABLATE & 1 the walk is skipped (timing-only builds).
+// interleaved for ILP).
 template <int N>
 __device__ __forceinline__ void mt_walk397xn(uint32_t (&x)[N]) {
 #pragma unroll
   for (int k = 0; k < N; ++k) x[k] = mt_seed_step(x[k], 1);
-#if !(YK_ABLATE & 1)
+#if YK_WALK_MAD
+  uint32_t cmul;
+  asm("v_mov_b32 %0, 0x6c078965" : "=v"(cmul));  // 1812433253
+#pragma unroll 4
+  for (uint32_t i = 2; i <= kMtM; ++i) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = mt_seed_step_mad(x[k], (uint64_t)i, cmul);
+  }
+#else
 #pragma unroll 4
   for (uint32_t i = 2; i <= kMtM; ++i) {
 #pragma unroll

@@ -42,6 +42,7 @@
 #include "yk_bvh.hpp"
 #include "yk_device.hpp"
 #include "yk_device_f32.hpp"
+#include "yk_stamps.hpp"
 
 using ykd::v3;
 
@@ -105,43 +106,14 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #ifndef YK_RENDER_PRIO
 #define YK_RENDER_PRIO 1
 #endif
-// YK_WIDE: 4-wide BVH nodes (ykbvh::WideNode); 0 = the binary slab nodes (A/B timing)
-#ifndef YK_WIDE
-#define YK_WIDE 1
-#endif
-#if YK_WIDE
-using DevNode = ykbvh::WideNode;
-#else
-using DevNode = ykbvh::SlabNode;
-#endif
-constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (diagnostic builds), [24..31]: work
-
-// Diagnostic build (YK_ABLATE & 8): per-wave s_memtime stamps at the loop's reconvergence
-// points, summed per phase into counters[8..13] (refill, start, traversal, candidates, shade,
-// path end).
-#if YK_ABLATE & 8
-#define YK_STAMP(k)                                                                  \
-  do {                                                                               \
-    uint64_t t_;                                                                     \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    st_acc[k] += t_ - st_prev;                                                       \
-    st_prev = t_;                                                                    \
-  } while (0)
-#else
-#define YK_STAMP(k) \
-  do {              \
-  } while (0)
-#endif
+using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
+constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
 
 #ifndef YK_CLAIM
 #define YK_CLAIM 512
 #endif
 constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
-#define YK_STR2(x) #x
-#define YK_STR(x) YK_STR2(x)
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
@@ -267,7 +239,6 @@ __device__ __forceinline__ float safe_rcp(float x) {
 // n / a for a root (sphere.hpp:36-38), a's refined reciprocal shared by all candidates; a wave
 // with any lane out of range takes the full division (divs_fast's rule)
 __device__ __forceinline__ double root_div(double n, double a, double ra, bool a_ok) {
-  if (!YK_DIVFAST) return n / a;
   double q = ykd::div_by(n, a, ra);
   if (__builtin_expect(__ballot(!(a_ok && ykd::num_range(n))) != 0, 0)) q = n / a;
   return q;
@@ -416,22 +387,13 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
 
 // A sample's colour record: r, g, b as one aligned 32-byte record per sample slot (one 16-byte
-// and one 8-byte store, the whole record in one 32-byte sector; YK_COL_AOS=0: 24-byte records,
-// three 8-byte stores).  yk_reduce_samples reads the records of consecutive slots, coalesced.
-#ifndef YK_COL_AOS
-#define YK_COL_AOS 1
-#endif
-constexpr size_t kColStride = YK_COL_AOS ? 4 : 3;
+// and one 8-byte store, the whole record in one 32-byte sector).  yk_reduce_samples reads the
+// records of consecutive slots, coalesced.
+constexpr size_t kColStride = 4;
 __device__ __forceinline__ void colour_store(double* col, uint32_t slot, double r, double g, double b) {
-#if YK_COL_AOS
   double* rec = col + (size_t)slot * kColStride;
   *(double2*)rec = make_double2(r, g);
   rec[2] = b;
-#else
-  col[(size_t)slot * kColStride + 0] = r;
-  col[(size_t)slot * kColStride + 1] = g;
-  col[(size_t)slot * kColStride + 2] = b;
-#endif
 }
 
 // Ordered sum of a launch's sample colours per pixel: pixel_color of source.cpp:137-167 is the
@@ -609,12 +571,7 @@ void yk_render_persistent(KernelArgs ka) {
   uint32_t n_dpos = 0;  // leaf tests with disc >= 0 (their root bounds are computed)
   uint32_t n_lamb = 0, n_metal = 0, n_fuzz = 0, n_diel = 0;  // hits shaded per material kind
 
-#if YK_ABLATE & 8
-  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t st_diag0 = 0;  // leaf tests with disc >= 0
-  uint64_t st_prev = __builtin_amdgcn_s_memtime();
-  if (lane == 0) atomicMin(&ka.counters[16], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
+  YK_STAMPS_BEGIN(ka.counters, lane);
   uint32_t slot = 0, depth = 0, nstk = 0;
   uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // newest attenuation id in st0's low half
   v3 o = {0, 0, 0}, d = {0, 0, 0};
@@ -625,9 +582,7 @@ void yk_render_persistent(KernelArgs ka) {
   for (;;) {
     // ---- refill (claim_slots): lanes without a path take the next sample slots
     if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) {
-#if YK_ABLATE & 8
-      atomicMin(&ka.counters[17], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
+      YK_STAMPS_EXHAUSTED(ka.counters);
       break;
     }
     YK_STAMP(0);
@@ -644,7 +599,7 @@ void yk_render_persistent(KernelArgs ka) {
       const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
       qpix = ka.order[slot - sl * ka.npix_slots];
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
-        const uint4* rp = (const uint4*)ka.start + 3u * ((YK_ABLATE & 128) ? (slot & 1023u) : slot);
+        const uint4* rp = (const uint4*)ka.start + 3u * slot;
         rq0 = rp[0];
         rq1 = rp[1];
         rq2 = rp[2];
@@ -667,7 +622,6 @@ void yk_render_persistent(KernelArgs ka) {
       double uc = 0, vc = 0, px = 0, py = 0;
       bool pre = false;
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
-        // (YK_ABLATE & 128, timing only: records from a 1024-slot window, always L2-resident)
         StartRec r;  // (loaded above with the pixel)
         __builtin_memcpy((char*)&r, &rq0, 16);
         __builtin_memcpy((char*)&r + 16, &rq1, 16);
@@ -756,19 +710,11 @@ void yk_render_persistent(KernelArgs ka) {
           iz = safe_rcp(dzf);
         }
         const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
-#if YK_WIDE
         // this ray's (near x4, far x4) plane quads inside a WideNode (yk_bvh.hpp), as base
         // pointers: a visit then costs one address add per axis
         const char* const px = nodes + (ix < 0.0f ? 16u : 0u);
         const char* const py = nodes + 48u + (iy < 0.0f ? 16u : 0u);
         const char* const pz = nodes + 96u + (iz < 0.0f ? 16u : 0u);
-#else
-        // this ray's (near, far) plane pairs inside a SlabNode (yk_bvh.hpp), as base pointers:
-        // a visit then costs one address add per axis
-        const char* const px = nodes + (ix < 0.0f ? 8u : 0u);
-        const char* const py = nodes + 24u + (iy < 0.0f ? 8u : 0u);
-        const char* const pz = nodes + 48u + (iz < 0.0f ? 8u : 0u);
-#endif
         // Conservative interval test without per-visit relaxation: far distances
         // come out of the FMA already scaled by c = 1 + 2^-17 (scaled 1/d and o/d), near
         // distances are compared unscaled against tmin_lo = t_min (1 - 2^-17) and against
@@ -800,25 +746,12 @@ void yk_render_persistent(KernelArgs ka) {
         // divergent exit has to merge (-3.4% as a bool), an integer flag is one more loop-carried
         // register (nc = 5 instead: -0.8%)
         int32_t node = ka.bvh_root;
-#if YK_WIDE
         int32_t* top = stk;  // this lane's traversal stack top (entries kBlk words apart)
         const int32_t* const stk_cap = stk + ka.stack_cap * kBlk;
-#else
-        uint32_t sp = 0;
-#endif
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
-#ifdef YK_NOPPAD
-            // diagnostic: YK_NOPPAD extra VALU issue slots per node visit (results unchanged)
-            asm volatile(".rept " YK_STR(YK_NOPPAD) "\n\tv_nop\n\t.endr" ::: "memory");
-#endif
-#if YK_ABLATE & 8
-            // wave-level iterations of the interior-node loop (diagnostic): the first active
-            // lane counts
-            if ((uint32_t)__builtin_ctzll(__ballot(1)) == lane) ++st_acc[7];
-#endif
-#if YK_WIDE
+            YK_STAMP_NODE_ITERATION(lane);
             // near / far distances of the 4 slots per axis, one packed FMA per pair of slots:
             // t = plane*(1/d) - o*(1/d), the binary node's arithmetic per slot
             const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
@@ -861,44 +794,9 @@ void yk_render_persistent(KernelArgs ka) {
               }
               continue;
             }
-#else
-            // near / far distances of both children per axis, one packed FMA per pair:
-            // t = plane*(1/d) - o*(1/d)
-            const char* const ax = px + node;
-            const f2 nx = __builtin_elementwise_fma(*(const f2*)(ax), ixv, noix);
-            const f2 fx = __builtin_elementwise_fma(*(const f2*)(ax + 8), ixc, noixc);
-            const f2 ny = __builtin_elementwise_fma(*(const f2*)(py + node), iyv, noiy);
-            const f2 fy = __builtin_elementwise_fma(*(const f2*)(py + node + 8), iyc, noiyc);
-            const f2 nz = __builtin_elementwise_fma(*(const f2*)(pz + node), izv, noiz);
-            const f2 fz = __builtin_elementwise_fma(*(const f2*)(pz + node + 8), izc, noizc);
-            const int2 ch = *(const int2*)(nodes + node + 72);
-            float tn[2];
-            bool hk[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              tn[k] = fmaxf(fmaxf(fmaxf(nx[k], ny[k]), nz[k]), tmin_lo);
-              const float tf = fminf(fminf(fminf(fx[k], fy[k]), fz[k]), ustar_f);
-              hk[k] = tn[k] <= tf;
-            }
-            const bool h0 = hk[0], h1 = hk[1];
-            if (h0 && h1) {
-              const bool first0 = tn[0] <= tn[1];
-              stk[sp * kBlk] = first0 ? ch.y : ch.x;
-              ++sp;
-              node = first0 ? ch.x : ch.y;
-              continue;
-            }
-            if (h0 || h1) {
-              node = h0 ? ch.x : ch.y;
-              continue;
-            }
-#endif
           } else {
             YK_STAMP(2);  // interior nodes since the last stamp
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
-#ifdef YK_LEAF_UNROLL
-#pragma unroll YK_LEAF_UNROLL
-#endif
             for (uint32_t k = 0; k < cnt; ++k) {
               const SphereGeo sg = leaf_geo[first + k];
               // the tuple index read with the geometry: its latency then hides under the
@@ -913,9 +811,7 @@ void yk_render_persistent(KernelArgs ka) {
               const double disc = hb * hb - a * c;
               if (disc < 0) continue;
               if (kCount) ++n_dpos;
-#if YK_ABLATE & 8
-              ++st_diag0;
-#endif
+              YK_STAMP_DISC_POS();
               // bounds of the exact root: |approx - exact| <= m (256x the error bound, §4)
               const double sq = ykd::sqrt_bound(disc);
               const double r1 = (-hb - sq) * ia, r2 = (-hb + sq) * ia;
@@ -953,15 +849,9 @@ void yk_render_persistent(KernelArgs ka) {
             }
             YK_STAMP(6);  // this leaf
           }
-#if YK_WIDE
           if (top == stk) break;
           top -= kBlk;
           node = *top;
-#else
-          if (sp == 0) break;
-          --sp;
-          node = stk[sp * kBlk];
-#endif
         }
         YK_STAMP(2);
         if (nc > 4) {
@@ -1128,7 +1018,7 @@ void yk_render_persistent(KernelArgs ka) {
         --nstk;
         return id;
       };
-      while (!(YK_ABLATE & 32) && nstk > 0) {
+      while (nstk > 0) {
         const SphereMat m = mat[pop()];
         L_r = m.ar * L_r;
         L_g = m.ag * L_g;
@@ -1136,21 +1026,13 @@ void yk_render_persistent(KernelArgs ka) {
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
       // the sample's colour; yk_reduce_samples adds them in sample order
-      if (!(YK_ABLATE & 64)) {
-        colour_store(ka.col, slot, L_r, L_g, L_b);
-      }
+      colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
     YK_STAMP(5);
   }
 
-#if YK_ABLATE & 8
-  if (lane == 0)
-    for (int k = 0; k < 7; ++k) atomicAdd(&ka.counters[8 + k], (unsigned long long)st_acc[k]);
-  atomicAdd(&ka.counters[15], (unsigned long long)st_acc[7]);  // per-lane partial counts
-  atomicAdd(&ka.counters[19], (unsigned long long)st_diag0);
-  if (lane == 0) atomicMax(&ka.counters[18], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
+  YK_STAMPS_END(ka.counters, lane);
   if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
     atomicAdd(&ka.counters[1], (unsigned long long)n_test);
@@ -1329,9 +1211,8 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
       const float onorm = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
       // the tree serves the rays its bound is proven for: |d|^2 in [2^-60, 2^60],
       // origin within origin_bound (< 0: the scene is outside the proven scale); the rest scan
-      bool linear = (ka.flags & kFlagLinearScan) || !YK_WIDE || !(a >= 0x1p-60f && a <= 0x1p60f) ||
+      bool linear = (ka.flags & kFlagLinearScan) || !(a >= 0x1p-60f && a <= 0x1p60f) ||
                     !((double)onorm <= ka.origin_bound);
-#if YK_WIDE
       if (!linear) {
         f2 inx, ncx, jfx, fcx, iny, ncy, jfy, fcy, inz, ncz, jfz, fcz;
         const float s = __builtin_sqrtf(a) * ykbvh::kF32Cone;  // the cone's slope (>= kF32Cone |d|)
@@ -1408,7 +1289,6 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
         }
         if (overflow != 0) linear = true;
       }
-#endif
       if (linear) {  // the reference's ordered scan in tuple order (wave-uniform scalar loads)
         ++n_lin;
         T = INFINITY;
@@ -2184,14 +2064,9 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   for (uint32_t i = 0; i < count; ++i)
     std::memcpy(leaf_geo.data() + i * elem, (const char*)geo + (size_t)bvh.order[i] * elem, elem);
   t.release();
-#if YK_WIDE
   int32_t root_code = 0;
   uint32_t wdepth = 0;
   const std::vector<DevNode> snodes = ykbvh::wide_nodes(bvh, &root_code, &wdepth);
-#else
-  const std::vector<DevNode> snodes = ykbvh::slab_nodes(bvh);
-  const int32_t root_code = ykbvh::slab_root(bvh);
-#endif
   const size_t nn = std::max<size_t>(1, snodes.size());
   YK_HIP(hipMalloc(&t.nodes, nn * sizeof(DevNode)));
   YK_HIP(hipMalloc(&t.leaf_geo, count * elem));
@@ -2226,7 +2101,6 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
     const size_t min_stacks = (size_t)12 * blk * 4;
     pl.in_lds = scene_bytes + tgeo_bytes + mat_bytes + min_stacks <= budget;
     const size_t tables = pl.in_lds ? tgeo_bytes + mat_bytes : 0;
-#if YK_WIDE
     // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries);
     // the capacity is what still fits the budget (at least 8); a lane that would exceed it
     // abandons the traversal for the exact linear scan.  Pushes write unconditionally at the
@@ -2237,10 +2111,6 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
       pl.stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
       pl.stack_entries = pl.stack_cap + 4;
     }
-#else
-    pl.stack_cap = bvh.depth + 1;
-    pl.stack_entries = bvh.depth + 1;
-#endif
     pl.tgeo_off = pl.in_lds && tgeo_elem ? (uint32_t)scene_bytes : 0u;
     pl.mat_off = pl.in_lds && tgeo_elem ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
     pl.stack_off = pl.in_lds ? (uint32_t)(scene_bytes + tables) : 0u;
