@@ -212,7 +212,7 @@ __device__ __forceinline__ void mt_start_from(MtLane& g, uint32_t seed, uint32_t
 }
 
 #ifndef YK_WALK_MAD
-#define YK_WALK_MAD 0
+#define YK_WALK_MAD 1
 #endif
 // One seeding step whose index is wave-uniform (the walk's loop counter, in SGPRs): the multiply
 // and the add of i as ONE v_mad_u64_u32 (low word of t * 1812433253 + i), three instructions
