@@ -5,7 +5,9 @@ launch c's draining blocks free), so rocprofv3's per-dispatch average counts the
 twice.  This reports, for the dispatches whose name contains the substring: the plain average
 span (what --stats prints), the UNION of the spans, and union / dispatches — the figure bench.py
 divides by (`roofline.launch_ms`).
-usage: python tools/kernel_union.py <run_kernel_trace.csv> [kernel-substring] [out.json]
+usage: python tools/kernel_union.py <run_kernel_trace.csv> [kernel-substring[|substring...]] [out.json]
+Several substrings ('|'-separated) take the union of all their dispatches (kernels that share a
+launch); "launches" = the dispatches of the LAST substring (one per launch).
 """
 import csv
 import json
@@ -15,8 +17,11 @@ import sys
 def main():
     path = sys.argv[1]
     kern = sys.argv[2] if len(sys.argv) > 2 else "yk_render_persistent<true, 0>"
+    names = kern.split("|")
+    rows = list(csv.DictReader(open(path)))
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
-                for r in csv.DictReader(open(path)) if kern in r["Kernel_Name"])
+                for r in rows if any(k in r["Kernel_Name"] for k in names))
+    launches = sum(1 for r in rows if names[-1] in r["Kernel_Name"])
     if not iv:
         raise SystemExit(f"no dispatch of {kern!r} in {path}")
     union = 0
@@ -29,9 +34,9 @@ def main():
             cur_e = max(cur_e, e)
     union += cur_e - cur_s
     spans = sum(e - s for s, e in iv)
-    out = {"trace": path, "kernel": kern, "dispatches": len(iv),
+    out = {"trace": path, "kernel": kern, "dispatches": len(iv), "launches": launches,
            "avg_span_ms": spans / len(iv) / 1e6, "union_ms": union / 1e6,
-           "union_per_dispatch_ms": union / len(iv) / 1e6,
+           "union_per_dispatch_ms": union / max(1, launches) / 1e6,
            "overlap_fraction_of_spans": 1 - union / spans}
     js = json.dumps(out, indent=1)
     if len(sys.argv) > 3:

@@ -1,7 +1,10 @@
 """Summarise tools/pmc_profile.sh output for one kernel: counters per dispatch and derived
 metrics (gfx950 corrections per MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half of a wide
 stream; GRBM_GUI_ACTIVE sums the 8 XCDs; SQ_* cycle counters are quad-cycles).
-usage: python tools/pmc_summary.py <pmc dir> [kernel-substring] [workload-tag] [out.json]"""
+usage: python tools/pmc_summary.py <pmc dir> [kernel-substring[|substring...]] [workload-tag] [out.json]
+Several '|'-separated substrings (kernels that share a launch) sum their counters; "per dispatch"
+then means per dispatch of the LAST one (one per launch).
+VALU busy / lane utilisation / the wait fractions come from the summed counters too."""
 import collections
 import csv
 import glob
@@ -12,19 +15,21 @@ import sys
 d = sys.argv[1]
 kern = sys.argv[2] if len(sys.argv) > 2 else "yk_render_persistent"
 workload = sys.argv[3] if len(sys.argv) > 3 else None
+names = kern.split("|")
 agg = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 dur = []
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        if kern in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in names):
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
+            if names[-1] in r["Kernel_Name"]:
+                disp[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_kernel_trace.csv"))):
     for r in csv.DictReader(open(f)):
-        if kern in r["Kernel_Name"]:
+        if names[-1] in r["Kernel_Name"]:
             dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-per = {k: v / len(disp[k]) for k, v in agg.items()}
+per = {k: v / max(1, len(disp[k])) for k, v in agg.items()}
 out = {"source": f"rocprofv3 --kernel-trace --pmc (4 passes), {d}", "kernel": kern,
        "workload": workload, "dispatches_profiled": len(dur),
        "mean_ms": sum(dur) / max(1, len(dur)), "counters_per_dispatch": per}
