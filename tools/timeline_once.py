@@ -18,5 +18,5 @@ with yk.Renderer(0) as r:
     print("---- timed call", file=sys.stderr, flush=True)
     r.render(p)
     st = r.stats()
-    print({k: st[k] for k in ("total_ms", "kernel_ms", "render_busy_ms", "warmup_ms", "resolve_ms", "primary_ms",
+    print({k: st[k] for k in ("total_ms", "kernel_ms", "render_busy_ms", "warmup_ms", "resolve_ms",
                               "launches")}, flush=True)

@@ -312,13 +312,15 @@ struct WarmArgs {
 template <bool kStart, bool kLens>
 __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
   constexpr int K = kStart ? YK_WARM_K : 4;  // samples per thread, interleaved
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * K;
-  for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * K; i0 < wa.n; i0 += stride) {
+  // (32-bit indices: a launch keeps its slots below 2^31 and the grid below 2^21 threads)
+  const uint32_t n = (uint32_t)wa.n;
+  const uint32_t stride = gridDim.x * blockDim.x * K;
+  for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * K; i0 < n; i0 += stride) {
     uint32_t x[K], seed[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const uint64_t i = i0 + k < wa.n ? i0 + k : wa.n - 1;
-      const uint32_t sl = fdiv((uint32_t)i, wa.nps_m, wa.nps_sh), pp = (uint32_t)i - sl * wa.npix_slots;
+      const uint32_t i = i0 + k < n ? i0 + k : n - 1;
+      const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
       const uint32_t q = wa.order[pp];
       const uint32_t pix = q == kNoPixel ? 0u : q;
       const uint32_t sm = wa.s0 + sl;
@@ -329,54 +331,44 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
     ykd::mt_walk397xn<K>(x);
     if constexpr (!kStart) {
       uint32_t* out = (uint32_t*)wa.out;
-      if (i0 + 4 <= wa.n) {
+      if (i0 + 4 <= n) {
         *(uint4*)(out + i0) = make_uint4(x[0], x[1], x[2], x[3]);
       } else {
-        for (int k = 0; k < 4 && i0 + k < wa.n; ++k) out[i0 + k] = x[k];
+        for (int k = 0; k < 4 && i0 + k < n; ++k) out[i0 + k] = x[k];
       }
     } else {
-      // the four samples' draws interleaved (independent cursor chains: ILP for the quarter-rate
-      // multiplies of the seeding recurrence)
-      StartRec r[K];
-      ykd::MtLane g[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        g[k].state = nullptr;
-        ykd::mt_start_from(g[k], seed[k], x[k]);
+      // the sample's start draws with the lazy cursors; the record is stored in three 16-byte
+      // pieces as soon as each is known (the jitter pair before the lens loop: its four
+      // registers are free during the loop).  22 VGPRs with a lens (30 before): with the three
+      // 128-VGPR render waves of a SIMD (384 of its 512) FIVE of these waves fit beside them
+      // (VGPRs are granted in granules of 8), where 32 allowed four
+      static_assert(K == 1, "StartRec warm-up: one sample per thread");
+      ykd::MtLane g;
+      g.state = nullptr;
+      ykd::mt_start_from(g, seed[0], x[0]);
+      const bool in = i0 < n;
+      uint4* const out = (uint4*)wa.out + 3 * (size_t)i0;
+      {
+        const double uc = ykd::canonical<true>(g);  // source.cpp:162: (x + dist(gen)) / W
+        const double vc = ykd::canonical<true>(g);  // source.cpp:163
+        if (in) *(double2*)out = make_double2(uc, vc);
       }
-#pragma unroll
-      for (int k = 0; k < K; ++k) r[k].uc = ykd::canonical<true>(g[k]);  // source.cpp:162: (x + dist(gen)) / W
-#pragma unroll
-      for (int k = 0; k < K; ++k) r[k].vc = ykd::canonical<true>(g[k]);  // source.cpp:163
-      uint32_t pending = 0;  // bit k: sample k still rejecting lens points
-      uint32_t failed = 0;   // bit k: the lens loop would reach the scratch engine's words
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        r[k].px = r[k].py = 0.0;
-        if (kLens) pending |= 1u << k;
-      }
-      while (pending) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          if (!(pending & (1u << k))) continue;
-          if (!ykd::rng_lazy_ok(g[k], 4)) {
-            failed |= 1u << k;
-            pending &= ~(1u << k);
-            continue;
+      double px = 0.0, py = 0.0;
+      bool failed = false;  // the lens loop would reach the scratch engine's words
+      if (kLens) {
+        for (;;) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
+          if (!ykd::rng_lazy_ok(g, 4)) {
+            failed = true;
+            break;
           }
-          r[k].px = ykd::uniform<true>(g[k], -1, 1);
-          r[k].py = ykd::uniform<true>(g[k], -1, 1);
-          if (r[k].px * r[k].px + r[k].py * r[k].py < 1.0) pending &= ~(1u << k);
+          px = ykd::uniform<true>(g, -1, 1);
+          py = ykd::uniform<true>(g, -1, 1);
+          if (px * px + py * py < 1.0) break;
         }
       }
-      StartRec* out = (StartRec*)wa.out;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        r[k].a0 = g[k].a0;
-        r[k].a1 = g[k].a1;
-        r[k].b = g[k].b;
-        r[k].j = (failed & (1u << k)) ? kNoStart : g[k].j;
-        if (i0 + k < wa.n) out[i0 + k] = r[k];
+      if (in) {
+        *(double2*)(out + 1) = make_double2(px, py);
+        out[2] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
       }
     }
   }
