@@ -29,6 +29,7 @@ __device__ __forceinline__ v3 neg(v3 a) { return {-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  // vec3.hpp:145-147
 __device__ __forceinline__ float len2(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }      // vec3.hpp:129
 __device__ __forceinline__ v3 of(const double* p) { return {(float)p[0], (float)p[1], (float)p[2]}; }
+__device__ __forceinline__ v3 off(const float* p) { return {p[0], p[1], p[2]}; }
 
 // math::sqrt<float> (math.hpp:10-19): `T x = s / 2.0` and `x = (x + s / x) / 2.0` halve in
 // double and round to float, which equals the float product by 0.5f (halving is exact, so both

@@ -118,8 +118,15 @@ constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
 
+// the camera rounded to float once on the host (camera<float>'s members, camera.hpp:10-27), and
+// W, H as floats: the FP32 kernel's start converts nothing
+struct CamF {
+  float origin[3], llc[3], horizontal[3], vertical[3], lens_u[3], lens_v[3];
+  float lens_radius, w, h, pad[3];
+};
 struct KernelArgs {
   yk_camera cam;
+  CamF camf;
   uint32_t W, H, spp, max_depth;
   uint32_t seed0, row_begin, row_count, row_stride, band_log2;
   uint32_t nspheres, pad_n, flags, id_stride;
@@ -309,7 +316,9 @@ struct WarmArgs {
 #ifndef YK_WARM_K
 #define YK_WARM_K 1
 #endif
-template <bool kStart, bool kLens>
+// kF32 (with kStart): the FP32 kernel's start — one-word float canonicals (ykf::canonical), the
+// same record layout (the floats held exactly as doubles)
+template <bool kStart, bool kLens, bool kF32 = false>
 __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
   constexpr int K = kStart ? YK_WARM_K : 4;  // samples per thread, interleaved
   // (32-bit indices: a launch keeps its slots below 2^31 and the grid below 2^21 threads)
@@ -348,7 +357,11 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       ykd::mt_start_from(g, seed[0], x[0]);
       const bool in = i0 < n;
       uint4* const out = (uint4*)wa.out + 3 * (size_t)i0;
-      {
+      if constexpr (kF32) {
+        const float uc = ykf::canonical<true>(g);  // source.cpp:162 with T = float
+        const float vc = ykf::canonical<true>(g);  // source.cpp:163
+        if (in) *(double2*)out = make_double2((double)uc, (double)vc);
+      } else {
         const double uc = ykd::canonical<true>(g);  // source.cpp:162: (x + dist(gen)) / W
         const double vc = ykd::canonical<true>(g);  // source.cpp:163
         if (in) *(double2*)out = make_double2(uc, vc);
@@ -357,13 +370,21 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       bool failed = false;  // the lens loop would reach the scratch engine's words
       if (kLens) {
         for (;;) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
-          if (!ykd::rng_lazy_ok(g, 4)) {
+          if (!ykd::rng_lazy_ok(g, kF32 ? 2 : 4)) {
             failed = true;
             break;
           }
-          px = ykd::uniform<true>(g, -1, 1);
-          py = ykd::uniform<true>(g, -1, 1);
-          if (px * px + py * py < 1.0) break;
+          if constexpr (kF32) {
+            const float fx = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
+            const float fy = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
+            px = fx;
+            py = fy;
+            if (fx * fx + fy * fy < 1.0f) break;
+          } else {
+            px = ykd::uniform<true>(g, -1, 1);
+            py = ykd::uniform<true>(g, -1, 1);
+            if (px * px + py * py < 1.0) break;
+          }
         }
       }
       if (in) {
@@ -455,13 +476,15 @@ __global__ __launch_bounds__(256) void yk_math_sqrt(const double* in, double* ou
 // are independent, only their SUM is ordered, and yk_reduce_samples does that.)  Returns true
 // when this lane has no path and the launch has no slots left: the lane exits.
 // The per-sample engine of a kernel instance (YK_RNG_*): lane set-up and the start of a sample.
-// mt19937 starts from the warm-up kernel's x_397 of the sample slot; xor128 needs only its seed.
+// mt19937 starts from the warm-up kernel's x_397 of the sample slot (the FP32 kernel built
+// without start records, YK_F32_START=0); xor128 needs only its seed.
 __device__ __forceinline__ void rng_init(ykd::MtLane& g, const KernelArgs& ka, uint32_t gid) {
   g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
   g.a0 = g.a1 = g.b = g.j = g.seed = 0;
 }
 __device__ __forceinline__ void rng_init(ykd::X128Lane& g, const KernelArgs&, uint32_t) { g.x = g.y = g.z = g.w = 0; }
-__device__ __forceinline__ void rng_start(ykd::MtLane& g, uint32_t seed, const KernelArgs& ka, uint32_t slot) {
+[[maybe_unused]] __device__ __forceinline__ void rng_start(ykd::MtLane& g, uint32_t seed, const KernelArgs& ka,
+                                                           uint32_t slot) {
   ykd::mt_start_from(g, seed, ka.warm[slot]);
 }
 __device__ __forceinline__ void rng_start(ykd::X128Lane& g, uint32_t seed, const KernelArgs&, uint32_t) {
@@ -1085,14 +1108,53 @@ __device__ __forceinline__ int f32_root(float4 sg, ykf::v3 o, ykf::v3 d, float a
   return 2;
 }
 
+#ifndef YK_F32_CAND
+#define YK_F32_CAND 1
+#endif
+#ifndef YK_F32_SLOW
+#define YK_F32_SLOW 1
+#endif
+#ifndef YK_F32_WARM_PER_CU
+#define YK_F32_WARM_PER_CU 2u
+#endif
+#ifndef YK_F32_START
+#define YK_F32_START 1
+#endif
+#ifndef YK_F32_CAP128
+#define YK_F32_CAP128 0
+#endif
+#ifndef YK_F32_FAR_AT
+#define YK_F32_FAR_AT (1.0f + 0x1p-10f)
+#endif
+
+// Bounds of the root f32_root returns, from the exact float discriminant: the
+// approximation r = (-hb ∓ v_sqrt_f32(disc)) · v_rcp_f32(a) differs from the exact root by at most
+// (|hb| + √disc)/a · 9u (one-step sqrt within 1.5u, v_sqrt/v_rcp within an ulp, three roundings;
+// u = 2^-24); m takes 256u, plus an absolute term for underflowing products.  A disc outside the
+// one-step square root's range [2^-100, 2^100] gets no bound (m = inf: always a candidate).
+// Returns false when both roots certainly lie below tmin; else lb <= the accepted root <= ub
+// (ub = inf when neither root is certainly >= tmin).  NaN anywhere keeps the sphere (every
+// comparison that would drop it is false).
+__device__ __forceinline__ bool f32_root_bounds(float hb, float disc, float ia, float tmin, float& lb, float& ub) {
+  const float sq = __builtin_amdgcn_sqrtf(disc);
+  const float r1 = (-hb - sq) * ia, r2 = (-hb + sq) * ia;
+  float m = (fabsf(hb) + sq) * ia * 0x1p-16f + 0x1p-120f;
+  if (!(disc >= 0x1p-100f && disc <= 0x1p100f)) m = INFINITY;
+  if (r2 + m < tmin) return false;
+  lb = fmaxf(tmin, r1 - m);
+  ub = (r1 - m >= tmin) ? r1 + m : ((r2 - m >= tmin) ? r2 + m : INFINITY);
+  return true;
+}
+
 // One axis of the ray's cone: near planes are crossed at (plane - o) * in, far
 // planes at (plane - o) * jf, with in = 1/(d + s sign d) and jf = (1 + 2^-17)/(d - s sign d); an
-// axis with |d| < 2s keeps no far bound (jf = 0, constant +inf).  Slab FMA operands: plane * in +
-// nc.  Culling arithmetic only: v_rcp_f32's ulp is inside the relative margins.
+// axis with |d| < YK_F32_FAR_AT * s keeps no far bound (jf = 0, constant +inf).  Slab FMA operands:
+// plane * in + nc.  Culling arithmetic only: v_rcp_f32's ulp is inside the relative margins (d - s
+// sign d is exact for |d| <= 2s, Sterbenz).
 __device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, f2& nc2, f2& jf2, f2& fc2) {
   const float sg = dk < 0.0f ? -s : s;
   const float in = __builtin_amdgcn_rcpf(dk + sg);
-  const bool far = fabsf(dk) >= 2.0f * s;
+  const bool far = fabsf(dk) >= YK_F32_FAR_AT * s;
   const float jf = far ? __builtin_amdgcn_rcpf(dk - sg) * (1.0f + 0x1p-17f) : 0.0f;
   const float nc = -(ok * in), fc = far ? -(ok * jf) : INFINITY;
   in2 = f2{in, in};
@@ -1105,7 +1167,13 @@ __device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, 
 // workgroup, as in the FP64 kernel.  kMode bit 0: the work counters; bit 2: the yk::xor128
 // engine (as for the FP64 kernel)
 template <bool kSceneInLds, int kMode>
-__global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs ka) {
+__global__ __launch_bounds__(mode_block<kMode>())
+#if YK_F32_CAP128
+__attribute__((amdgpu_waves_per_eu((kMode & 1) ? 1 : 4, 8)))
+#elif defined(YK_F32_WPE)
+__attribute__((amdgpu_waves_per_eu(YK_F32_WPE, YK_F32_WPE)))
+#endif
+void yk_render_f32(KernelArgs ka) {
   constexpr int kBlk = mode_block<kMode>();
   constexpr bool kCount = (kMode & 1) != 0;
   using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
@@ -1144,6 +1212,7 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
   rng_init(g, ka, gid);
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_nit = 0, n_ncall = 0, n_node = 0, n_lin = 0;
+  YK_STAMPS_BEGIN(ka.counters, lane);
   const float tmin = (float)ka.t_min;  // world.hit(r, 0.001, ...) converts to T (hittable.hpp:32)
   uint32_t slot = 0, depth = 0, nstk = 0;
   uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
@@ -1152,37 +1221,87 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
   uint32_t res_base = 0, res_left = 0;
 
   for (;;) {
-    if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) break;
+    if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) {
+      YK_STAMPS_EXHAUSTED(ka.counters);
+      break;
+    }
+    YK_STAMP(0);
 
     // ---- start: seed, jitter, camera<float>::get_ray (source.cpp:154-165, camera.hpp:29-32)
     bool start = !in_path;
     uint32_t qpix = 0;
+#if YK_F32_START
+    // mt19937: the start's draws come precomputed (yk_mt_warmup<true, lens, true>: StartRec with
+    // float canonicals), loaded with the pixel as in the FP64 kernel
+    constexpr bool kRec = std::is_same<Gen, ykd::MtLane>::value;
+#else
+    constexpr bool kRec = false;
+#endif
+    uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0};
     if (start) {
       const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
       qpix = ka.order[slot - sl * ka.npix_slots];
+      if constexpr (kRec) {
+        const uint4* rp = (const uint4*)ka.start + 3u * slot;
+        rq0 = rp[0];
+        rq1 = rp[1];
+        rq2 = rp[2];
+        asm volatile("" ::"v"(rq0.x), "v"(rq0.y), "v"(rq0.z), "v"(rq0.w), "v"(rq1.x), "v"(rq1.y),
+                     "v"(rq1.z), "v"(rq1.w), "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(qpix));
+      }
       start = qpix != kNoPixel;
     }
     if (start) {
       const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
       const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
-      rng_start(g, ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s), ka, slot);
+      const uint32_t seed = ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
+      const bool lens = ka.cam.lens_radius > 0;  // (decided in double, as for the warm-up)
+      float uc = 0, vc = 0, px = 0, py = 0;
+      bool pre = false;
+      if constexpr (kRec) {
+        StartRec r;
+        __builtin_memcpy((char*)&r, &rq0, 16);
+        __builtin_memcpy((char*)&r + 16, &rq1, 16);
+        __builtin_memcpy((char*)&r + 32, &rq2, 16);
+        pre = r.j != kNoStart;
+        if (pre) {
+          g.seed = seed;
+          g.a0 = r.a0;
+          g.a1 = r.a1;
+          g.b = r.b;
+          g.j = r.j;
+          uc = (float)r.uc;
+          vc = (float)r.vc;
+          px = (float)r.px;
+          py = (float)r.py;
+        }
+      }
+      if (!pre) {
+        if constexpr (kRec)
+          rng_start_full(g, seed);
+        else
+          rng_start(g, seed, ka, slot);
+        uc = f_uniform01(g);
+        vc = f_uniform01(g);
+        if (lens) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
+          do {
+            px = ykf::uniform(g, -1.0f, 1.0f);
+            py = ykf::uniform(g, -1.0f, 1.0f);
+          } while (!(px * px + py * py < 1.0f));
+        }
+      }
       // (x + U01) / W with x, W unsigned → float (uniform_real_distribution<float>)
-      const float u = ((float)x + f_uniform01(g)) / (float)ka.W;
-      const float v = ((float)(ka.H - y - 1) + f_uniform01(g)) / (float)ka.H;
-      const ykf::v3 cam_o = ykf::of(ka.cam.origin), cam_llc = ykf::of(ka.cam.lower_left_corner);
-      const ykf::v3 cam_h = ykf::of(ka.cam.horizontal), cam_v = ykf::of(ka.cam.vertical);
+      const float u = ((float)x + uc) / ka.camf.w;
+      const float v = ((float)(ka.H - y - 1) + vc) / ka.camf.h;
+      const ykf::v3 cam_o = ykf::off(ka.camf.origin), cam_llc = ykf::off(ka.camf.llc);
+      const ykf::v3 cam_h = ykf::off(ka.camf.horizontal), cam_v = ykf::off(ka.camf.vertical);
       d = ykf::sub(ykf::add(ykf::add(cam_llc, ykf::mul(cam_h, u)), ykf::mul(cam_v, v)), cam_o);
       o = cam_o;
-      if (ka.cam.lens_radius > 0) {  // thin-lens extension
-        float px, py;
-        do {
-          px = ykf::uniform(g, -1.0f, 1.0f);
-          py = ykf::uniform(g, -1.0f, 1.0f);
-        } while (!(px * px + py * py < 1.0f));
-        const float lr = (float)ka.cam.lens_radius;
+      if (lens) {
+        const float lr = ka.camf.lens_radius;
         const float rx = px * lr, ry = py * lr;
-        const ykf::v3 off = ykf::add(ykf::mul(ykf::of(ka.cam.lens_u), rx), ykf::mul(ykf::of(ka.cam.lens_v), ry));
+        const ykf::v3 off = ykf::add(ykf::mul(ykf::off(ka.camf.lens_u), rx), ykf::mul(ykf::off(ka.camf.lens_v), ry));
         o = ykf::add(o, off);
         d = ykf::sub(d, off);
       }
@@ -1191,6 +1310,7 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
       in_path = true;
     }
 
+    YK_STAMP(1);
     if (kCount && (ka.flags & kFlagTrace) && in_path) trace_ray(ka, slot, ka.max_depth - depth, o, d);
 
     // ---- closest hit (hittable_list.hpp:32-58 over sphere.hpp:25-48, in float)
@@ -1215,8 +1335,40 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
         const char* const px = nodes + (d.x < 0.0f ? 16u : 0u);
         const char* const py = nodes + 48u + (d.y < 0.0f ? 16u : 0u);
         const char* const pz = nodes + 96u + (d.z < 0.0f ? 16u : 0u);
+#if YK_F32_SLOW
+        // A slow axis (|d| < s, the cone opens both ways along it) has no far bound, but the cone
+        // still enters a box that lies against the direction of travel only after its far-side
+        // plane: o + (d - s sign d) t reaches it at t = (plane - o) / (d - s sign d) > 0, a lower
+        // bound like a near distance (same FMA form and error).  Without it, a
+        // ray grazing a field of boxes enters every box under its path.  One slow axis per ray
+        // gets the bound (y, then x, then z); the others keep L = -inf.
+        f2 jl2 = {0.0f, 0.0f}, cl2 = {-INFINITY, -INFINITY};
+        const char* pl = px + 16;
+        {
+          const float slow = s * (1.0f - 0x1p-10f);
+          const float dk[3] = {d.z, d.x, d.y}, ok[3] = {o.z, o.x, o.y};
+          const char* const pk[3] = {pz, px, py};
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            if (fabsf(dk[k]) < slow) {
+              const float jl = __builtin_amdgcn_rcpf(dk[k] - (dk[k] < 0.0f ? -s : s));
+              jl2 = f2{jl, jl};
+              cl2 = f2{-(ok[k] * jl), -(ok[k] * jl)};
+              pl = pk[k] + 16;
+            }
+          }
+        }
+#endif
         const float tmin_lo = tmin * (1.0f - 0x1p-17f);
         float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
+#if YK_F32_CAND
+        // U*: proven upper bound of the minimum root (culls with ustar_f = U* (1 + 2^-18)); the
+        // candidate list (tuple index, lower bound) as in the FP64 kernel, nc = 5 on overflow
+        const float ia = __builtin_amdgcn_rcpf(a);  // a in [2^-60, 2^60] here
+        float ustar = INFINITY;
+        uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+#endif
         uint32_t overflow = 0;  // a VGPR, not a lane-mask bool (see the FP64 kernel)
         int32_t node = ka.bvh_root;
         int32_t* top = stk;
@@ -1224,6 +1376,7 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
+            YK_STAMP_NODE_ITERATION(lane);
             // the FP64 kernel's visit (same planes, margins and visit order), the cone's operands
             const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
             const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
@@ -1235,10 +1388,20 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
             const f2 fy[2] = {__builtin_elementwise_fma(qfy.xy, jfy, fcy), __builtin_elementwise_fma(qfy.zw, jfy, fcy)};
             const f2 nz[2] = {__builtin_elementwise_fma(qnz.xy, inz, ncz), __builtin_elementwise_fma(qnz.zw, inz, ncz)};
             const f2 fz[2] = {__builtin_elementwise_fma(qfz.xy, jfz, fcz), __builtin_elementwise_fma(qfz.zw, jfz, fcz)};
+#if YK_F32_SLOW
+            const f4 qsl = *(const f4*)(pl + node);
+            const f2 sl[2] = {__builtin_elementwise_fma(qsl.xy, jl2, cl2), __builtin_elementwise_fma(qsl.zw, jl2, cl2)};
+#endif
             bool hk[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
+#if YK_F32_SLOW
+              // (a chain: two v_max3)
+              const float tn = fmaxf(fmaxf(fmaxf(fmaxf(nx[k >> 1][k & 1], ny[k >> 1][k & 1]), nz[k >> 1][k & 1]),
+                                           sl[k >> 1][k & 1]), tmin_lo);
+#else
               const float tn = fmaxf(fmaxf(fmaxf(nx[k >> 1][k & 1], ny[k >> 1][k & 1]), nz[k >> 1][k & 1]), tmin_lo);
+#endif
               const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
@@ -1259,7 +1422,49 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
               continue;
             }
           } else {
+            YK_STAMP(2);
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
+#if YK_F32_CAND
+            // bound-then-evaluate, as in the FP64 kernel: the exact discriminant decides disc < 0,
+            // the root gets bounds only, and the survivors' exact roots are evaluated after the
+            // traversal, with the lanes converged
+            for (uint32_t k = 0; k < cnt; ++k) {
+              const float4 sg = leaf_geo[first + k];
+              const uint32_t id = leaf_ids[first + k];
+              asm volatile("" ::"v"(id));
+              if (kCount) ++n_test;
+              const ykf::v3 oc = {o.x - sg.x, o.y - sg.y, o.z - sg.z};
+              const float hb = ykf::dot(oc, d);
+              const float c = ykf::len2(oc) - sg.w;
+              const float disc = hb * hb - a * c;
+              if (disc < 0) continue;
+              YK_STAMP_DISC_POS();
+              float lb, ub;
+              if (!f32_root_bounds(hb, disc, ia, tmin, lb, ub)) continue;
+              if (!(lb <= ustar)) continue;
+              if (ub < ustar) {
+                ustar = ub;
+                ustar_f = ub * (1.0f + 0x1p-18f);
+              }
+              if (nc == 4) {  // compact: drop entries the new bound has excluded
+                uint32_t m2 = 0;
+                uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
+                float e0 = l0, e1 = l1, e2 = l2, e3 = l3;
+                if (e0 <= ustar) { YK_CAND_SET(m2, d0, e0); ++m2; }
+                if (e1 <= ustar) { YK_CAND_SET(m2, d1, e1); ++m2; }
+                if (e2 <= ustar) { YK_CAND_SET(m2, d2, e2); ++m2; }
+                if (e3 <= ustar) { YK_CAND_SET(m2, d3, e3); ++m2; }
+                nc = m2;
+              }
+              if (nc < 4) {
+                c3 = c2, l3 = l2, c2 = c1, l2 = l1, c1 = c0, l1 = l0;
+                c0 = id, l0 = lb;
+                ++nc;
+              } else {
+                nc = 5;  // the list is full: the ordered scan decides
+              }
+            }
+#else
             for (uint32_t k = 0; k < cnt; ++k) {
               if (kCount) ++n_test;
               float r = 0.0f;
@@ -1274,12 +1479,35 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
                 ustar_f = r * (1.0f + 0x1p-18f);
               }
             }
+#endif
+            YK_STAMP(6);
           }
           if (top == stk) break;
           top -= kBlk;
           node = *top;
         }
+        YK_STAMP(2);
         if (overflow != 0) linear = true;
+#if YK_F32_CAND
+        if (nc > 4) linear = true;
+        if (!linear) {
+          // the survivors' exact roots: the minimum wins, an exact tie goes to the later tuple
+          // index (hittable_list.hpp:36-43); a candidate whose lower bound exceeds the final U*
+          // cannot be the minimum
+#define YK_F32_EVAL(C, L)                                                       \
+  if ((L) <= ustar) {                                                           \
+    float r = 0.0f;                                                             \
+    const int res = f32_root(geo_f[C], o, d, a, tmin, r, n_nit);                \
+    if (kCount && res > 0) ++n_sqrt, ++n_ncall;                                 \
+    if (res == 2 && (r < T || (r == T && (int)(C) > hid))) T = r, hid = (int)(C); \
+  }
+          if (nc > 0) YK_F32_EVAL(c0, l0)
+          if (nc > 1) YK_F32_EVAL(c1, l1)
+          if (nc > 2) YK_F32_EVAL(c2, l2)
+          if (nc > 3) YK_F32_EVAL(c3, l3)
+#undef YK_F32_EVAL
+        }
+#endif
       }
       if (linear) {  // the reference's ordered scan in tuple order (wave-uniform scalar loads)
         ++n_lin;
@@ -1306,6 +1534,7 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
       }
     }
 
+    YK_STAMP(3);
     // ---- shade (raytracer.hpp:25-36, material.hpp), material-uniform as in the FP64 kernel: one
     //      block of canonicals (float: one word each) for lambertian's vec3::random (3), the fuzzed
     //      metal's factor and vector (4) and the dielectric's uniform (1, drawn speculatively and
@@ -1417,6 +1646,7 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
       }
     }
 
+    YK_STAMP(4);
     if (ended) {
       // attenuation (double albedo) back to front, as in FP64 (raytracer.hpp:31)
       while (nstk > 0) {
@@ -1435,7 +1665,9 @@ __global__ __launch_bounds__(mode_block<kMode>()) void yk_render_f32(KernelArgs 
       colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
+    YK_STAMP(5);
   }
+  YK_STAMPS_END(ka.counters, lane);
   if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
     atomicAdd(&ka.counters[1], (unsigned long long)n_test);
@@ -1719,6 +1951,17 @@ uint32_t reduce_blocks(const ykgpu_context* ctx, uint32_t nps) {
   return cap ? std::max(1u, std::min(full, cap)) : full;
 }
 
+// Warm-up grid: grid-stride, at most `per_cu` blocks (one wave per SIMD each) per CU
+// (YKGPU_WARM_PER_CU overrides).  The FP64 StartRec warm-up is close to the render's critical
+// path and takes every idle issue slot it can (32; 16: neutral, 8: +1.8%); the FP32 one has
+// slack, and each resident warm-up wave delays the latency-bound render waves it shares a SIMD
+// with (512-spp FP32 A/B: 32 -> 205.2 ms, 4 -> 202.4, 3 -> 202.4, 2 -> 201.3)
+uint32_t warm_per_cu(bool f32) {
+  uint32_t per_cu = f32 ? YK_F32_WARM_PER_CU : 32u;
+  if (const char* e = std::getenv("YKGPU_WARM_PER_CU")) per_cu = (uint32_t)std::max(1, std::atoi(e));
+  return per_cu;
+}
+
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
   const bool f32 = p->precision == YK_PRECISION_FP32;
@@ -1787,7 +2030,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   };
   const uint32_t nlaunch = (uint32_t)sched.size();
   // warm-up records: the FP64 kernel's whole sample start (StartRec), the FP32 kernel's x_397
-  const size_t welem = f32 ? sizeof(uint32_t) : sizeof(StartRec);
+  // per sample: x_397 (FP32 without start records) or a StartRec
+  const bool f32_walk = f32 && !YK_F32_START;
+  const size_t welem = f32_walk ? sizeof(uint32_t) : sizeof(StartRec);
   const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (welem * nps * K)));
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
@@ -1798,6 +2043,21 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
+  {
+    const yk_camera& c = ctx->cam;
+    for (int k = 0; k < 3; ++k) {
+      ka.camf.origin[k] = (float)c.origin[k];
+      ka.camf.llc[k] = (float)c.lower_left_corner[k];
+      ka.camf.horizontal[k] = (float)c.horizontal[k];
+      ka.camf.vertical[k] = (float)c.vertical[k];
+      ka.camf.lens_u[k] = (float)c.lens_u[k];
+      ka.camf.lens_v[k] = (float)c.lens_v[k];
+      ka.camf.pad[k] = 0.0f;
+    }
+    ka.camf.lens_radius = (float)c.lens_radius;
+    ka.camf.w = (float)p->image_width;  // unsigned → float (source.cpp:162, T = float)
+    ka.camf.h = (float)p->image_height;
+  }
   ka.W = p->image_width;
   ka.H = p->image_height;
   ka.spp = p->samples_per_pixel;
@@ -1905,11 +2165,15 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     wa.s0 = sched[c].first;
     wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
-    const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * 32);
+    const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * warm_per_cu(f32));
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
-      if (f32)
+      if (f32_walk)
         hipLaunchKernelGGL((yk_mt_warmup<false, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      else if (f32 && wa.lens)
+        hipLaunchKernelGGL((yk_mt_warmup<true, true, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      else if (f32)
+        hipLaunchKernelGGL((yk_mt_warmup<true, false, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else if (wa.lens)
         hipLaunchKernelGGL((yk_mt_warmup<true, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else
@@ -1931,8 +2195,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.nsl = nsl;
     ka.col = col;
     char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
-    ka.warm = f32 ? (const uint32_t*)wring : nullptr;
-    ka.start = f32 ? nullptr : (const void*)wring;
+    ka.warm = f32_walk ? (const uint32_t*)wring : nullptr;
+    ka.start = f32_walk ? nullptr : (const void*)wring;
     // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
     // only on its own x_397 and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
