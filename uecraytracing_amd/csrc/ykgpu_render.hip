@@ -136,8 +136,8 @@ struct KernelArgs {
   uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
   uint64_t seed_key;
   const uint32_t* __restrict__ order;  // p → tile pixel (kNoPixel: empty slot of an edge block)
-  const uint32_t* __restrict__ warm;   // x_397 per sample slot of the launch (FP32 mt19937 kernel)
-  const void* __restrict__ start;      // StartRec per sample slot (FP64 mt19937 kernel)
+  uint64_t pad_a;                      // (keeps the argument layout the kernels were tuned with)
+  const void* __restrict__ start;      // StartRec per sample slot (mt19937 kernels)
   double t_min;
   double inv_w, inv_h;  // RN(1/W), RN(1/H) for the camera's exact divisions (div_markstein)
   double w_d, h_d;      // W, H as doubles (kernel arguments: no loop-hoisted conversion to hold)
@@ -280,7 +280,7 @@ __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; 
 // neighbouring pixels in both directions.  Every pixel's samples are independent of the order.
 constexpr uint32_t kNoPixel = 0xffffffffu;
 
-// A sample's start, precomputed by yk_mt_warmup<true, lens> for the FP64 mt19937 kernel: the two
+// A sample's start, precomputed by yk_mt_warmup<lens, f32> for the mt19937 kernels: the two
 // jitter canonicals (source.cpp:162-163), the accepted thin-lens point (random_in_unit_disk by
 // rejection; 0 without a lens) and the lazy cursors after those draws (x_j, x_{j+1}, x_{j+397},
 // j).  j == kNoStart: the lens loop would have reached the scratch engine's words (never seen:
@@ -292,14 +292,16 @@ struct alignas(16) StartRec {
 static_assert(sizeof(StartRec) == 48, "StartRec layout");
 constexpr uint32_t kNoStart = 0xffffffffu;
 
-// Seed walk of every sample of a launch, fully coherent: K consecutive samples per thread.
-// kStart = false: out[i] = x_397(seed(i)) (four samples per thread, one 16-B store; the FP32
-// kernel's engines); kStart = true: a StartRec per sample — the walk, then the start's own draws
-// with the lazy cursors (yk_device.hpp), which thereby leave the divergent render loop; kLens:
-// the camera has a lens (the rejection loop is compiled only then: its registers cost
-// co-resident waves).  The walk is ~400 dependent steps of xor-shift, v_mul_lo_u32 and add per
-// sample (8.9e12 steps/s on the whole GPU, tools/walkbench.hip: 47 ms of a 512-spp frame if it
-// ran alone), so these waves live on the render's idle issue cycles at lower priority.
+// Seed walk and start draws of every sample of a launch, fully coherent, one sample per thread
+// (grid-stride): a StartRec per sample — the 397-step walk, then the start's own draws with the
+// lazy cursors (yk_device.hpp), which thereby leave the divergent render loop.  kLens: the camera
+// has a lens (the rejection loop is compiled only then: its registers cost co-resident waves);
+// kF32: the FP32 kernel's start (one-word float canonicals, ykf::canonical; the same layout, the
+// floats held exactly as doubles).  The walk is ~400 dependent steps per sample (8.9e12 steps/s
+// on the whole GPU, tools/walkbench.hip: 47 ms of a 512-spp frame if it ran alone), so these
+// waves live on the render's idle issue cycles at lower priority.  One sample per thread (two or
+// four interleaved: 204.6 -> 211.2 / 215.5 ms, 512-spp A/B) keeps the kernel at 22 VGPRs with a
+// lens: beside the three 128-VGPR render waves of a SIMD (384 of its 512) five of its waves fit.
 struct WarmArgs {
   uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode, band_log2;
   uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
@@ -310,88 +312,58 @@ struct WarmArgs {
   void* out;
 };
 
-// YK_WARM_K samples per thread, interleaved.  One: the StartRec kernel then needs 26 VGPRs (30
-// with a lens), so four of its waves fit beside the three render waves of each SIMD (512-spp A/B:
-// 4 -> 215.5 ms, 2 -> 211.2, 1 -> 204.6; with the render at 128 VGPRs, 1 -> 202.4)
-#ifndef YK_WARM_K
-#define YK_WARM_K 1
-#endif
-// kF32 (with kStart): the FP32 kernel's start — one-word float canonicals (ykf::canonical), the
-// same record layout (the floats held exactly as doubles)
-template <bool kStart, bool kLens, bool kF32 = false>
+template <bool kLens, bool kF32>
 __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
-  constexpr int K = kStart ? YK_WARM_K : 4;  // samples per thread, interleaved
   // (32-bit indices: a launch keeps its slots below 2^31 and the grid below 2^21 threads)
   const uint32_t n = (uint32_t)wa.n;
-  const uint32_t stride = gridDim.x * blockDim.x * K;
-  for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * K; i0 < n; i0 += stride) {
-    uint32_t x[K], seed[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint32_t i = i0 + k < n ? i0 + k : n - 1;
-      const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
-      const uint32_t q = wa.order[pp];
-      const uint32_t pix = q == kNoPixel ? 0u : q;
-      const uint32_t sm = wa.s0 + sl;
-      const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh), xx = pix - tr * wa.W;
-      const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
-      x[k] = seed[k] = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, sm);
-    }
-    ykd::mt_walk397xn<K>(x);
-    if constexpr (!kStart) {
-      uint32_t* out = (uint32_t*)wa.out;
-      if (i0 + 4 <= n) {
-        *(uint4*)(out + i0) = make_uint4(x[0], x[1], x[2], x[3]);
-      } else {
-        for (int k = 0; k < 4 && i0 + k < n; ++k) out[i0 + k] = x[k];
-      }
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
+    const uint32_t q = wa.order[pp];
+    const uint32_t pix = q == kNoPixel ? 0u : q;
+    const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh), xx = pix - tr * wa.W;
+    const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
+    const uint32_t seed = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
+    uint32_t x[1] = {seed};
+    ykd::mt_walk397xn<1>(x);
+    // the start draws; the record is stored in three 16-byte pieces as soon as each is known
+    // (the jitter pair before the lens loop: its four registers are free during the loop)
+    ykd::MtLane g;
+    g.state = nullptr;
+    ykd::mt_start_from(g, seed, x[0]);
+    uint4* const out = (uint4*)wa.out + 3 * (size_t)i;
+    if constexpr (kF32) {
+      const float uc = ykf::canonical<true>(g);  // source.cpp:162 with T = float
+      const float vc = ykf::canonical<true>(g);  // source.cpp:163
+      *(double2*)out = make_double2((double)uc, (double)vc);
     } else {
-      // the sample's start draws with the lazy cursors; the record is stored in three 16-byte
-      // pieces as soon as each is known (the jitter pair before the lens loop: its four
-      // registers are free during the loop).  22 VGPRs with a lens (30 before): with the three
-      // 128-VGPR render waves of a SIMD (384 of its 512) FIVE of these waves fit beside them
-      // (VGPRs are granted in granules of 8), where 32 allowed four
-      static_assert(K == 1, "StartRec warm-up: one sample per thread");
-      ykd::MtLane g;
-      g.state = nullptr;
-      ykd::mt_start_from(g, seed[0], x[0]);
-      const bool in = i0 < n;
-      uint4* const out = (uint4*)wa.out + 3 * (size_t)i0;
-      if constexpr (kF32) {
-        const float uc = ykf::canonical<true>(g);  // source.cpp:162 with T = float
-        const float vc = ykf::canonical<true>(g);  // source.cpp:163
-        if (in) *(double2*)out = make_double2((double)uc, (double)vc);
-      } else {
-        const double uc = ykd::canonical<true>(g);  // source.cpp:162: (x + dist(gen)) / W
-        const double vc = ykd::canonical<true>(g);  // source.cpp:163
-        if (in) *(double2*)out = make_double2(uc, vc);
-      }
-      double px = 0.0, py = 0.0;
-      bool failed = false;  // the lens loop would reach the scratch engine's words
-      if (kLens) {
-        for (;;) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
-          if (!ykd::rng_lazy_ok(g, kF32 ? 2 : 4)) {
-            failed = true;
-            break;
-          }
-          if constexpr (kF32) {
-            const float fx = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
-            const float fy = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
-            px = fx;
-            py = fy;
-            if (fx * fx + fy * fy < 1.0f) break;
-          } else {
-            px = ykd::uniform<true>(g, -1, 1);
-            py = ykd::uniform<true>(g, -1, 1);
-            if (px * px + py * py < 1.0) break;
-          }
+      const double uc = ykd::canonical<true>(g);  // source.cpp:162: (x + dist(gen)) / W
+      const double vc = ykd::canonical<true>(g);  // source.cpp:163
+      *(double2*)out = make_double2(uc, vc);
+    }
+    double px = 0.0, py = 0.0;
+    bool failed = false;  // the lens loop would reach the scratch engine's words
+    if (kLens) {
+      for (;;) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
+        if (!ykd::rng_lazy_ok(g, kF32 ? 2 : 4)) {
+          failed = true;
+          break;
+        }
+        if constexpr (kF32) {
+          const float fx = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
+          const float fy = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
+          px = fx;
+          py = fy;
+          if (fx * fx + fy * fy < 1.0f) break;
+        } else {
+          px = ykd::uniform<true>(g, -1, 1);
+          py = ykd::uniform<true>(g, -1, 1);
+          if (px * px + py * py < 1.0) break;
         }
       }
-      if (in) {
-        *(double2*)(out + 1) = make_double2(px, py);
-        out[2] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
-      }
     }
+    *(double2*)(out + 1) = make_double2(px, py);
+    out[2] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
   }
 }
 
@@ -475,23 +447,14 @@ __global__ __launch_bounds__(256) void yk_math_sqrt(const double* in, double* ou
 // res_left) stays wave-uniform.  (A pixel is not a lane's unit of work: the samples of a pixel
 // are independent, only their SUM is ordered, and yk_reduce_samples does that.)  Returns true
 // when this lane has no path and the launch has no slots left: the lane exits.
-// The per-sample engine of a kernel instance (YK_RNG_*): lane set-up and the start of a sample.
-// mt19937 starts from the warm-up kernel's x_397 of the sample slot (the FP32 kernel built
-// without start records, YK_F32_START=0); xor128 needs only its seed.
+// The per-sample engine of a kernel instance (YK_RNG_*): lane set-up.
 __device__ __forceinline__ void rng_init(ykd::MtLane& g, const KernelArgs& ka, uint32_t gid) {
   g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
   g.a0 = g.a1 = g.b = g.j = g.seed = 0;
 }
 __device__ __forceinline__ void rng_init(ykd::X128Lane& g, const KernelArgs&, uint32_t) { g.x = g.y = g.z = g.w = 0; }
-[[maybe_unused]] __device__ __forceinline__ void rng_start(ykd::MtLane& g, uint32_t seed, const KernelArgs& ka,
-                                                           uint32_t slot) {
-  ykd::mt_start_from(g, seed, ka.warm[slot]);
-}
-__device__ __forceinline__ void rng_start(ykd::X128Lane& g, uint32_t seed, const KernelArgs&, uint32_t) {
-  ykd::x128_start(g, seed);
-}
 
-// A sample's engine from its seed alone (the FP64 kernel's start when no StartRec serves it):
+// A sample's engine from its seed alone (xor128, and an mt19937 start no StartRec serves):
 // mt19937 walks its 397 seeding steps here
 __device__ __forceinline__ void rng_start_full(ykd::MtLane& g, uint32_t seed) { ykd::mt_start(g, seed); }
 __device__ __forceinline__ void rng_start_full(ykd::X128Lane& g, uint32_t seed) { ykd::x128_start(g, seed); }
@@ -631,7 +594,7 @@ void yk_render_persistent(KernelArgs ka) {
       const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
       const double lens_r = ka.cam.lens_radius;
       // The start's draws — the two jitter canonicals, then the lens point — and the engine after
-      // them: precomputed for mt19937 by yk_mt_warmup<true> (StartRec), so the divergent loop
+      // them: precomputed for mt19937 by yk_mt_warmup (StartRec), so the divergent loop
       // only loads them; xor128, and the (never seen) record the warm-up could not complete,
       // draw here
       double uc = 0, vc = 0, px = 0, py = 0;
@@ -1079,13 +1042,14 @@ RenderKernel fp64_kernel(bool lds, int mode) {
 }
 
 // ---- render<float> (YK_PRECISION_FP32) ---------------------------------------------------
-// The same persistent, sample-parallel structure as yk_render_persistent (refill, slots, MT
-// cursors from yk_mt_warmup, attenuation-id stack, SoA colours reduced by yk_reduce_samples),
+// The same persistent, sample-parallel structure as yk_render_persistent (refill, slots, start
+// records from yk_mt_warmup, attenuation-id stack, SoA colours reduced by yk_reduce_samples),
 // with the path in float (yk_device_f32.hpp).  Closest hit: the FP32 tree culls — its boxes and
-// a per-ray cone carry the float sphere test's proven error — and every sphere
-// of an entered leaf gets the reference's float test itself (as cheap as bounds would be, so
-// there is no candidate stage): the minimum root wins, an exact tie goes to the later tuple
-// index.  Rays outside the tree's proven range take the ordered scan (hittable_list.hpp:32-58).
+// a per-ray cone carry the float sphere test's proven error — the spheres of an
+// entered leaf get the reference's float discriminant and bounds of their float root, and the
+// survivors' exact float roots are evaluated after the traversal: the minimum root wins, an exact
+// tie goes to the later tuple index.  Rays outside the tree's proven range take the ordered scan
+// (hittable_list.hpp:32-58).
 template <class G>
 __device__ __forceinline__ float f_uniform01(G& g) { return ykf::uniform(g, 0.0f, 1.0f); }
 
@@ -1108,24 +1072,9 @@ __device__ __forceinline__ int f32_root(float4 sg, ykf::v3 o, ykf::v3 d, float a
   return 2;
 }
 
-#ifndef YK_F32_CAND
-#define YK_F32_CAND 1
-#endif
-#ifndef YK_F32_SLOW
-#define YK_F32_SLOW 1
-#endif
-#ifndef YK_F32_WARM_PER_CU
-#define YK_F32_WARM_PER_CU 2u
-#endif
-#ifndef YK_F32_START
-#define YK_F32_START 1
-#endif
-#ifndef YK_F32_CAP128
-#define YK_F32_CAP128 0
-#endif
-#ifndef YK_F32_FAR_AT
-#define YK_F32_FAR_AT (1.0f + 0x1p-10f)
-#endif
+// the cone keeps a far bound on an axis with |d| >= kF32FarAt s, and gives the slow-axis bound
+// to one with |d| < kF32SlowAt s (d - s sign d stays clear of 0 in both)
+constexpr float kF32FarAt = 1.0f + 0x1p-10f, kF32SlowAt = 1.0f - 0x1p-10f;
 
 // Bounds of the root f32_root returns, from the exact float discriminant: the
 // approximation r = (-hb ∓ v_sqrt_f32(disc)) · v_rcp_f32(a) differs from the exact root by at most
@@ -1148,13 +1097,13 @@ __device__ __forceinline__ bool f32_root_bounds(float hb, float disc, float ia, 
 
 // One axis of the ray's cone: near planes are crossed at (plane - o) * in, far
 // planes at (plane - o) * jf, with in = 1/(d + s sign d) and jf = (1 + 2^-17)/(d - s sign d); an
-// axis with |d| < YK_F32_FAR_AT * s keeps no far bound (jf = 0, constant +inf).  Slab FMA operands:
+// axis with |d| < kF32FarAt s keeps no far bound (jf = 0, constant +inf).  Slab FMA operands:
 // plane * in + nc.  Culling arithmetic only: v_rcp_f32's ulp is inside the relative margins (d - s
 // sign d is exact for |d| <= 2s, Sterbenz).
 __device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, f2& nc2, f2& jf2, f2& fc2) {
   const float sg = dk < 0.0f ? -s : s;
   const float in = __builtin_amdgcn_rcpf(dk + sg);
-  const bool far = fabsf(dk) >= YK_F32_FAR_AT * s;
+  const bool far = fabsf(dk) >= kF32FarAt * s;
   const float jf = far ? __builtin_amdgcn_rcpf(dk - sg) * (1.0f + 0x1p-17f) : 0.0f;
   const float nc = -(ok * in), fc = far ? -(ok * jf) : INFINITY;
   in2 = f2{in, in};
@@ -1168,11 +1117,6 @@ __device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, 
 // engine (as for the FP64 kernel)
 template <bool kSceneInLds, int kMode>
 __global__ __launch_bounds__(mode_block<kMode>())
-#if YK_F32_CAP128
-__attribute__((amdgpu_waves_per_eu((kMode & 1) ? 1 : 4, 8)))
-#elif defined(YK_F32_WPE)
-__attribute__((amdgpu_waves_per_eu(YK_F32_WPE, YK_F32_WPE)))
-#endif
 void yk_render_f32(KernelArgs ka) {
   constexpr int kBlk = mode_block<kMode>();
   constexpr bool kCount = (kMode & 1) != 0;
@@ -1230,13 +1174,9 @@ void yk_render_f32(KernelArgs ka) {
     // ---- start: seed, jitter, camera<float>::get_ray (source.cpp:154-165, camera.hpp:29-32)
     bool start = !in_path;
     uint32_t qpix = 0;
-#if YK_F32_START
-    // mt19937: the start's draws come precomputed (yk_mt_warmup<true, lens, true>: StartRec with
+    // mt19937: the start's draws come precomputed (yk_mt_warmup<lens, true>: StartRec with
     // float canonicals), loaded with the pixel as in the FP64 kernel
     constexpr bool kRec = std::is_same<Gen, ykd::MtLane>::value;
-#else
-    constexpr bool kRec = false;
-#endif
     uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0};
     if (start) {
       const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
@@ -1278,10 +1218,7 @@ void yk_render_f32(KernelArgs ka) {
         }
       }
       if (!pre) {
-        if constexpr (kRec)
-          rng_start_full(g, seed);
-        else
-          rng_start(g, seed, ka, slot);
+        rng_start_full(g, seed);
         uc = f_uniform01(g);
         vc = f_uniform01(g);
         if (lens) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
@@ -1335,7 +1272,6 @@ void yk_render_f32(KernelArgs ka) {
         const char* const px = nodes + (d.x < 0.0f ? 16u : 0u);
         const char* const py = nodes + 48u + (d.y < 0.0f ? 16u : 0u);
         const char* const pz = nodes + 96u + (d.z < 0.0f ? 16u : 0u);
-#if YK_F32_SLOW
         // A slow axis (|d| < s, the cone opens both ways along it) has no far bound, but the cone
         // still enters a box that lies against the direction of travel only after its far-side
         // plane: o + (d - s sign d) t reaches it at t = (plane - o) / (d - s sign d) > 0, a lower
@@ -1345,7 +1281,7 @@ void yk_render_f32(KernelArgs ka) {
         f2 jl2 = {0.0f, 0.0f}, cl2 = {-INFINITY, -INFINITY};
         const char* pl = px + 16;
         {
-          const float slow = s * (1.0f - 0x1p-10f);
+          const float slow = s * kF32SlowAt;
           const float dk[3] = {d.z, d.x, d.y}, ok[3] = {o.z, o.x, o.y};
           const char* const pk[3] = {pz, px, py};
 #pragma unroll
@@ -1358,17 +1294,14 @@ void yk_render_f32(KernelArgs ka) {
             }
           }
         }
-#endif
         const float tmin_lo = tmin * (1.0f - 0x1p-17f);
         float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
-#if YK_F32_CAND
         // U*: proven upper bound of the minimum root (culls with ustar_f = U* (1 + 2^-18)); the
         // candidate list (tuple index, lower bound) as in the FP64 kernel, nc = 5 on overflow
         const float ia = __builtin_amdgcn_rcpf(a);  // a in [2^-60, 2^60] here
         float ustar = INFINITY;
         uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-#endif
         uint32_t overflow = 0;  // a VGPR, not a lane-mask bool (see the FP64 kernel)
         int32_t node = ka.bvh_root;
         int32_t* top = stk;
@@ -1388,20 +1321,14 @@ void yk_render_f32(KernelArgs ka) {
             const f2 fy[2] = {__builtin_elementwise_fma(qfy.xy, jfy, fcy), __builtin_elementwise_fma(qfy.zw, jfy, fcy)};
             const f2 nz[2] = {__builtin_elementwise_fma(qnz.xy, inz, ncz), __builtin_elementwise_fma(qnz.zw, inz, ncz)};
             const f2 fz[2] = {__builtin_elementwise_fma(qfz.xy, jfz, fcz), __builtin_elementwise_fma(qfz.zw, jfz, fcz)};
-#if YK_F32_SLOW
             const f4 qsl = *(const f4*)(pl + node);
             const f2 sl[2] = {__builtin_elementwise_fma(qsl.xy, jl2, cl2), __builtin_elementwise_fma(qsl.zw, jl2, cl2)};
-#endif
             bool hk[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-#if YK_F32_SLOW
               // (a chain: two v_max3)
               const float tn = fmaxf(fmaxf(fmaxf(fmaxf(nx[k >> 1][k & 1], ny[k >> 1][k & 1]), nz[k >> 1][k & 1]),
                                            sl[k >> 1][k & 1]), tmin_lo);
-#else
-              const float tn = fmaxf(fmaxf(fmaxf(nx[k >> 1][k & 1], ny[k >> 1][k & 1]), nz[k >> 1][k & 1]), tmin_lo);
-#endif
               const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
@@ -1424,7 +1351,6 @@ void yk_render_f32(KernelArgs ka) {
           } else {
             YK_STAMP(2);
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
-#if YK_F32_CAND
             // bound-then-evaluate, as in the FP64 kernel: the exact discriminant decides disc < 0,
             // the root gets bounds only, and the survivors' exact roots are evaluated after the
             // traversal, with the lanes converged
@@ -1464,22 +1390,6 @@ void yk_render_f32(KernelArgs ka) {
                 nc = 5;  // the list is full: the ordered scan decides
               }
             }
-#else
-            for (uint32_t k = 0; k < cnt; ++k) {
-              if (kCount) ++n_test;
-              float r = 0.0f;
-              const int res = f32_root(leaf_geo[first + k], o, d, a, tmin, r, n_nit);
-              if (kCount && res > 0) ++n_sqrt, ++n_ncall;
-              if (res < 2) continue;
-              // closest wins, an exact tie goes to the later tuple index (hittable_list.hpp:36-43)
-              const int id = (int)leaf_ids[first + k];
-              if (r < T || (r == T && id > hid)) {
-                T = r;
-                hid = id;
-                ustar_f = r * (1.0f + 0x1p-18f);
-              }
-            }
-#endif
             YK_STAMP(6);
           }
           if (top == stk) break;
@@ -1488,7 +1398,6 @@ void yk_render_f32(KernelArgs ka) {
         }
         YK_STAMP(2);
         if (overflow != 0) linear = true;
-#if YK_F32_CAND
         if (nc > 4) linear = true;
         if (!linear) {
           // the survivors' exact roots: the minimum wins, an exact tie goes to the later tuple
@@ -1507,7 +1416,6 @@ void yk_render_f32(KernelArgs ka) {
           if (nc > 3) YK_F32_EVAL(c3, l3)
 #undef YK_F32_EVAL
         }
-#endif
       }
       if (linear) {  // the reference's ordered scan in tuple order (wave-uniform scalar loads)
         ++n_lin;
@@ -1957,7 +1865,7 @@ uint32_t reduce_blocks(const ykgpu_context* ctx, uint32_t nps) {
 // slack, and each resident warm-up wave delays the latency-bound render waves it shares a SIMD
 // with (512-spp FP32 A/B: 32 -> 205.2 ms, 4 -> 202.4, 3 -> 202.4, 2 -> 201.3)
 uint32_t warm_per_cu(bool f32) {
-  uint32_t per_cu = f32 ? YK_F32_WARM_PER_CU : 32u;
+  uint32_t per_cu = f32 ? 2u : 32u;
   if (const char* e = std::getenv("YKGPU_WARM_PER_CU")) per_cu = (uint32_t)std::max(1, std::atoi(e));
   return per_cu;
 }
@@ -2030,9 +1938,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   };
   const uint32_t nlaunch = (uint32_t)sched.size();
   // warm-up records: the FP64 kernel's whole sample start (StartRec), the FP32 kernel's x_397
-  // per sample: x_397 (FP32 without start records) or a StartRec
-  const bool f32_walk = f32 && !YK_F32_START;
-  const size_t welem = f32_walk ? sizeof(uint32_t) : sizeof(StartRec);
+  const size_t welem = sizeof(StartRec);  // per sample slot
   const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (welem * nps * K)));
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
@@ -2043,6 +1949,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
+  ka.pad_a = 0;
   {
     const yk_camera& c = ctx->cam;
     for (int k = 0; k < 3; ++k) {
@@ -2070,7 +1977,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.nspheres = ctx->nspheres;
   ka.flags = p->flags;
   ka.id_stride = ctx->id_stride;
-  ka.warm = nullptr;
   ka.start = nullptr;
   ka.order = ctx->d_order;
   ka.t_min = p->t_min;
@@ -2168,16 +2074,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * warm_per_cu(f32));
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
-      if (f32_walk)
-        hipLaunchKernelGGL((yk_mt_warmup<false, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
-      else if (f32 && wa.lens)
-        hipLaunchKernelGGL((yk_mt_warmup<true, true, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
-      else if (f32)
-        hipLaunchKernelGGL((yk_mt_warmup<true, false, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
-      else if (wa.lens)
+      if (f32 && wa.lens)
         hipLaunchKernelGGL((yk_mt_warmup<true, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
-      else
+      else if (f32)
+        hipLaunchKernelGGL((yk_mt_warmup<false, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      else if (wa.lens)
         hipLaunchKernelGGL((yk_mt_warmup<true, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      else
+        hipLaunchKernelGGL((yk_mt_warmup<false, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       YK_HIP(hipGetLastError());
     }
     YK_HIP(hipEventRecord(ev[1], ctx->aux));
@@ -2195,8 +2099,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.nsl = nsl;
     ka.col = col;
     char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
-    ka.warm = f32_walk ? (const uint32_t*)wring : nullptr;
-    ka.start = f32_walk ? nullptr : (const void*)wring;
+    ka.start = (const void*)wring;
     // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
     // only on its own x_397 and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
