@@ -280,33 +280,81 @@ __device__ __forceinline__ v3 ld3(const double* p) { return {p[0], p[1], p[2]}; 
 // neighbouring pixels in both directions.  Every pixel's samples are independent of the order.
 constexpr uint32_t kNoPixel = 0xffffffffu;
 
-// A sample's start, precomputed by yk_mt_warmup<lens, f32> for the mt19937 kernels: the two
-// jitter canonicals (source.cpp:162-163), the accepted thin-lens point (random_in_unit_disk by
-// rejection; 0 without a lens) and the lazy cursors after those draws (x_j, x_{j+1}, x_{j+397},
-// j).  j == kNoStart: the lens loop would have reached the scratch engine's words (never seen:
-// ~55 rejections), and the render kernel starts that sample itself.
+// camera::get_ray (camera.hpp:29-32) for pixel (x, y) from the start's draws: the jitter
+// canonicals uc, vc (source.cpp:162-163, (x + U01) / W correctly rounded by Markstein's form with
+// the host's RN(1/W), yk_device.hpp) and the thin-lens point (px, py) when the camera has a lens.
+// The warm-up and the render kernel's own start (xor128, or a record the warm-up could not
+// complete) both call it, so a record's ray is the ray the render would have computed.
+__device__ __forceinline__ void camera_ray(const yk_camera& cam, double w_d, double inv_w, double h_d,
+                                           double inv_h, uint32_t H, uint32_t x, uint32_t y, double uc,
+                                           double vc, bool lens, double px, double py, v3& o, v3& d) {
+  const double u = ykd::div_markstein((double)x + ykd::uniform_of(uc, 0, 1), w_d, inv_w);
+  const double v = ykd::div_markstein((double)(H - y - 1) + ykd::uniform_of(vc, 0, 1), h_d, inv_h);
+  const v3 cam_o = ld3(cam.origin), cam_llc = ld3(cam.lower_left_corner);
+  const v3 cam_h = ld3(cam.horizontal), cam_v = ld3(cam.vertical);
+  d = ykd::sub(ykd::add(ykd::add(cam_llc, ykd::mul(cam_h, u)), ykd::mul(cam_v, v)), cam_o);
+  o = cam_o;
+  if (lens) {  // thin-lens offset
+    const double rx = px * cam.lens_radius, ry = py * cam.lens_radius;
+    const v3 off = ykd::add(ykd::mul(ld3(cam.lens_u), rx), ykd::mul(ld3(cam.lens_v), ry));
+    o = ykd::add(o, off);
+    d = ykd::sub(d, off);
+  }
+}
+// the same in float (camera<float>, the host-rounded camera CamF; (x + U01) / W a float division)
+__device__ __forceinline__ void camera_ray_f32(const CamF& cam, uint32_t H, uint32_t x, uint32_t y, float uc,
+                                               float vc, bool lens, float px, float py, ykf::v3& o, ykf::v3& d) {
+  const float u = ((float)x + uc) / cam.w;
+  const float v = ((float)(H - y - 1) + vc) / cam.h;
+  const ykf::v3 cam_o = ykf::off(cam.origin), cam_llc = ykf::off(cam.llc);
+  const ykf::v3 cam_h = ykf::off(cam.horizontal), cam_v = ykf::off(cam.vertical);
+  d = ykf::sub(ykf::add(ykf::add(cam_llc, ykf::mul(cam_h, u)), ykf::mul(cam_v, v)), cam_o);
+  o = cam_o;
+  if (lens) {
+    const float rx = px * cam.lens_radius, ry = py * cam.lens_radius;
+    const ykf::v3 off = ykf::add(ykf::mul(ykf::off(cam.lens_u), rx), ykf::mul(ykf::off(cam.lens_v), ry));
+    o = ykf::add(o, off);
+    d = ykf::sub(d, off);
+  }
+}
+
+// A sample's start, precomputed by yk_mt_warmup for the mt19937 kernels: the camera ray of the
+// sample (after the jitter canonicals and the thin-lens rejection loop) and the lazy cursors
+// after those draws (x_j, x_{j+1}, x_{j+397}, j).  j == kNoStart: the lens loop would have
+// reached the scratch engine's words (never seen: ~55 rejections), and the render kernel starts
+// that sample itself.  FP64: 64 bytes (four 16-byte loads); FP32: 48.
 struct alignas(16) StartRec {
-  double uc, vc, px, py;
+  double ox, oy, oz, dx, dy, dz;
   uint32_t a0, a1, b, j;
 };
-static_assert(sizeof(StartRec) == 48, "StartRec layout");
+static_assert(sizeof(StartRec) == 64, "StartRec layout");
+struct alignas(16) StartRecF {
+  float ox, oy, oz, dx, dy, dz;
+  uint32_t pad0, pad1;
+  uint32_t a0, a1, b, j;
+};
+static_assert(sizeof(StartRecF) == 48, "StartRecF layout");
 constexpr uint32_t kNoStart = 0xffffffffu;
 
-// Seed walk and start draws of every sample of a launch, fully coherent, one sample per thread
-// (grid-stride): a StartRec per sample — the 397-step walk, then the start's own draws with the
-// lazy cursors (yk_device.hpp), which thereby leave the divergent render loop.  kLens: the camera
-// has a lens (the rejection loop is compiled only then: its registers cost co-resident waves);
-// kF32: the FP32 kernel's start (one-word float canonicals, ykf::canonical; the same layout, the
-// floats held exactly as doubles).  The walk is ~400 dependent steps per sample (8.9e12 steps/s
-// on the whole GPU, tools/walkbench.hip: 47 ms of a 512-spp frame if it ran alone), so these
-// waves live on the render's idle issue cycles at lower priority.  One sample per thread (two or
-// four interleaved: 204.6 -> 211.2 / 215.5 ms, 512-spp A/B) keeps the kernel at 22 VGPRs with a
-// lens: beside the three 128-VGPR render waves of a SIMD (384 of its 512) five of its waves fit.
+// Seed walk and start of every sample of a launch, fully coherent, one sample per thread
+// (grid-stride): the 397-step walk, then the start's draws with the lazy cursors (yk_device.hpp)
+// and the camera ray, which thereby leave the divergent render loop.  kLens: the camera has a
+// lens (the rejection loop is compiled only then: its registers cost co-resident waves); kF32:
+// the FP32 kernel's start (one-word float canonicals, ykf::canonical; camera<float>).  The walk
+// is ~400 dependent steps per sample (8.9e12 steps/s on the whole GPU, tools/walkbench.hip: 47 ms
+// of a 512-spp frame if it ran alone), so these waves live on the render's idle issue cycles at
+// lower priority.  One sample per thread (two or four interleaved: 204.6 -> 211.2 / 215.5 ms,
+// 512-spp A/B): 32 VGPRs with a lens, so four of these waves fit beside the three 128-VGPR
+// render waves of a SIMD (a record of the draws instead of the ray: 20 VGPRs and five waves,
+// 0.5% slower, r03ab).
 struct WarmArgs {
   uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode, band_log2;
   uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
-  uint32_t lens, pad_w;               // the camera has a lens (lens_radius > 0)
+  uint32_t lens, H;                   // the camera has a lens (lens_radius > 0); image height
   uint64_t seed_key;
+  yk_camera cam;
+  CamF camf;
+  double w_d, h_d, inv_w, inv_h;      // as in KernelArgs
   const uint32_t* order;
   uint64_t n;  // sample slots in the launch
   void* out;
@@ -326,44 +374,54 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
     const uint32_t seed = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
     uint32_t x[1] = {seed};
     ykd::mt_walk397xn<1>(x);
-    // the start draws; the record is stored in three 16-byte pieces as soon as each is known
-    // (the jitter pair before the lens loop: its four registers are free during the loop)
     ykd::MtLane g;
     g.state = nullptr;
     ykd::mt_start_from(g, seed, x[0]);
-    uint4* const out = (uint4*)wa.out + 3 * (size_t)i;
+    bool failed = false;  // the lens loop would reach the scratch engine's words
     if constexpr (kF32) {
       const float uc = ykf::canonical<true>(g);  // source.cpp:162 with T = float
       const float vc = ykf::canonical<true>(g);  // source.cpp:163
-      *(double2*)out = make_double2((double)uc, (double)vc);
-    } else {
-      const double uc = ykd::canonical<true>(g);  // source.cpp:162: (x + dist(gen)) / W
-      const double vc = ykd::canonical<true>(g);  // source.cpp:163
-      *(double2*)out = make_double2(uc, vc);
-    }
-    double px = 0.0, py = 0.0;
-    bool failed = false;  // the lens loop would reach the scratch engine's words
-    if (kLens) {
-      for (;;) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
-        if (!ykd::rng_lazy_ok(g, kF32 ? 2 : 4)) {
-          failed = true;
-          break;
+      float px = 0.0f, py = 0.0f;
+      if (kLens) {
+        for (;;) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
+          if (!ykd::rng_lazy_ok(g, 2)) {
+            failed = true;
+            break;
+          }
+          px = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
+          py = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
+          if (px * px + py * py < 1.0f) break;
         }
-        if constexpr (kF32) {
-          const float fx = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
-          const float fy = ykf::uniform_of(ykf::canonical<true>(g), -1.0f, 1.0f);
-          px = fx;
-          py = fy;
-          if (fx * fx + fy * fy < 1.0f) break;
-        } else {
+      }
+      ykf::v3 o, d;
+      camera_ray_f32(wa.camf, wa.H, xx, y, uc, vc, kLens, px, py, o, d);
+      uint4* const out = (uint4*)wa.out + 3 * (size_t)i;
+      *(float4*)out = make_float4(o.x, o.y, o.z, d.x);
+      *(float4*)(out + 1) = make_float4(d.y, d.z, 0.0f, 0.0f);
+      out[2] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
+    } else {
+      const double uc = ykd::canonical<true>(g);  // source.cpp:162
+      const double vc = ykd::canonical<true>(g);  // source.cpp:163
+      double px = 0.0, py = 0.0;
+      if (kLens) {
+        for (;;) {
+          if (!ykd::rng_lazy_ok(g, 4)) {
+            failed = true;
+            break;
+          }
           px = ykd::uniform<true>(g, -1, 1);
           py = ykd::uniform<true>(g, -1, 1);
           if (px * px + py * py < 1.0) break;
         }
       }
+      v3 o, d;
+      camera_ray(wa.cam, wa.w_d, wa.inv_w, wa.h_d, wa.inv_h, wa.H, xx, y, uc, vc, kLens, px, py, o, d);
+      uint4* const out = (uint4*)wa.out + 4 * (size_t)i;
+      *(double2*)out = make_double2(o.x, o.y);
+      *(double2*)(out + 1) = make_double2(o.z, d.x);
+      *(double2*)(out + 2) = make_double2(d.y, d.z);
+      out[3] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
     }
-    *(double2*)(out + 1) = make_double2(px, py);
-    out[2] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
   }
 }
 
@@ -572,76 +630,63 @@ void yk_render_persistent(KernelArgs ka) {
     // one after the other they cost three dependent memory round trips per sample start (the
     // record's j, then its other words under the test).  Every slot of the launch, padded ones
     // included, has a record, so the read is in bounds.
-    uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0};
+    uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0}, rq3 = {0, 0, 0, 0};
     if (start) {
       const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
       qpix = ka.order[slot - sl * ka.npix_slots];
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
-        const uint4* rp = (const uint4*)ka.start + 3u * slot;
+        const uint4* rp = (const uint4*)ka.start + 4u * slot;
         rq0 = rp[0];
         rq1 = rp[1];
         rq2 = rp[2];
+        rq3 = rp[3];
         asm volatile("" ::"v"(rq0.x), "v"(rq0.y), "v"(rq0.z), "v"(rq0.w), "v"(rq1.x), "v"(rq1.y),
-                     "v"(rq1.z), "v"(rq1.w), "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(qpix));
+                     "v"(rq1.z), "v"(rq1.w), "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(rq3.x),
+                     "v"(rq3.y), "v"(rq3.z), "v"(rq3.w), "v"(qpix));
       }
       start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
     if (start) {
+      // The start — the jitter canonicals, the lens point and the camera ray — and the engine
+      // after its draws: precomputed for mt19937 by yk_mt_warmup (StartRec), so the divergent
+      // loop only loads them; xor128, and the (never seen) record the warm-up could not
+      // complete, start here
       const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
       const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       // seed (uint32 wrap, source.cpp:154-158)
       const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
-      const double lens_r = ka.cam.lens_radius;
-      // The start's draws — the two jitter canonicals, then the lens point — and the engine after
-      // them: precomputed for mt19937 by yk_mt_warmup (StartRec), so the divergent loop
-      // only loads them; xor128, and the (never seen) record the warm-up could not complete,
-      // draw here
-      double uc = 0, vc = 0, px = 0, py = 0;
       bool pre = false;
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
         StartRec r;  // (loaded above with the pixel)
         __builtin_memcpy((char*)&r, &rq0, 16);
         __builtin_memcpy((char*)&r + 16, &rq1, 16);
         __builtin_memcpy((char*)&r + 32, &rq2, 16);
+        __builtin_memcpy((char*)&r + 48, &rq3, 16);
         pre = r.j != kNoStart;
         if (pre) {
-          g.seed = seed;
+          g.seed = seed;  // (the scratch engine's seeding needs it)
           g.a0 = r.a0;
           g.a1 = r.a1;
           g.b = r.b;
           g.j = r.j;
-          uc = r.uc;
-          vc = r.vc;
-          px = r.px;
-          py = r.py;
+          o = v3{r.ox, r.oy, r.oz};
+          d = v3{r.dx, r.dy, r.dz};
         }
       }
       if (!pre) {
+        const bool lens = ka.cam.lens_radius > 0;
         rng_start_full(g, seed);
-        uc = ykd::canonical<true>(g);  // (a fresh engine: its first words never need the scratch engine)
-        vc = ykd::canonical<true>(g);
-        if (lens_r > 0) {  // thin-lens extension: random_in_unit_disk by rejection
+        const double uc = ykd::canonical<true>(g);  // (a fresh engine: its first words never need the scratch engine)
+        const double vc = ykd::canonical<true>(g);
+        double px = 0, py = 0;
+        if (lens) {  // thin-lens extension: random_in_unit_disk by rejection
           do {
             px = ykd::uniform(g, -1, 1);
             py = ykd::uniform(g, -1, 1);
           } while (!(px * px + py * py < 1.0));
         }
-      }
-      // (x + U01) / W and (H - y - 1 + U01) / H, correctly rounded (Markstein, yk_device.hpp)
-      const double u = ykd::div_markstein((double)x + ykd::uniform_of(uc, 0, 1), ka.w_d, ka.inv_w);
-      const double v = ykd::div_markstein((double)(ka.H - y - 1) + ykd::uniform_of(vc, 0, 1), ka.h_d, ka.inv_h);
-      // camera::get_ray (camera.hpp:29-32): llc + u*horizontal + v*vertical (- origin)
-      const v3 cam_o = ld3(ka.cam.origin), cam_llc = ld3(ka.cam.lower_left_corner);
-      const v3 cam_h = ld3(ka.cam.horizontal), cam_v = ld3(ka.cam.vertical);
-      d = ykd::sub(ykd::add(ykd::add(cam_llc, ykd::mul(cam_h, u)), ykd::mul(cam_v, v)), cam_o);
-      o = cam_o;
-      if (lens_r > 0) {  // thin-lens offset
-        const double rx = px * lens_r, ry = py * lens_r;
-        const v3 lens_u = ld3(ka.cam.lens_u), lens_v = ld3(ka.cam.lens_v);
-        const v3 off = ykd::add(ykd::mul(lens_u, rx), ykd::mul(lens_v, ry));
-        o = ykd::add(o, off);
-        d = ykd::sub(d, off);
+        camera_ray(ka.cam, ka.w_d, ka.inv_w, ka.h_d, ka.inv_h, ka.H, x, y, uc, vc, lens, px, py, o, d);
       }
       depth = ka.max_depth;
       nstk = 0;
@@ -1174,8 +1219,8 @@ void yk_render_f32(KernelArgs ka) {
     // ---- start: seed, jitter, camera<float>::get_ray (source.cpp:154-165, camera.hpp:29-32)
     bool start = !in_path;
     uint32_t qpix = 0;
-    // mt19937: the start's draws come precomputed (yk_mt_warmup<lens, true>: StartRec with
-    // float canonicals), loaded with the pixel as in the FP64 kernel
+    // mt19937: the start (draws and camera<float> ray) comes precomputed (yk_mt_warmup<lens,
+    // true>: StartRecF), loaded with the pixel as in the FP64 kernel
     constexpr bool kRec = std::is_same<Gen, ykd::MtLane>::value;
     uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0};
     if (start) {
@@ -1187,7 +1232,7 @@ void yk_render_f32(KernelArgs ka) {
         rq1 = rp[1];
         rq2 = rp[2];
         asm volatile("" ::"v"(rq0.x), "v"(rq0.y), "v"(rq0.z), "v"(rq0.w), "v"(rq1.x), "v"(rq1.y),
-                     "v"(rq1.z), "v"(rq1.w), "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(qpix));
+                     "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(qpix));
       }
       start = qpix != kNoPixel;
     }
@@ -1196,11 +1241,9 @@ void yk_render_f32(KernelArgs ka) {
       const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       const uint32_t seed = ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
-      const bool lens = ka.cam.lens_radius > 0;  // (decided in double, as for the warm-up)
-      float uc = 0, vc = 0, px = 0, py = 0;
       bool pre = false;
       if constexpr (kRec) {
-        StartRec r;
+        StartRecF r;
         __builtin_memcpy((char*)&r, &rq0, 16);
         __builtin_memcpy((char*)&r + 16, &rq1, 16);
         __builtin_memcpy((char*)&r + 32, &rq2, 16);
@@ -1211,36 +1254,23 @@ void yk_render_f32(KernelArgs ka) {
           g.a1 = r.a1;
           g.b = r.b;
           g.j = r.j;
-          uc = (float)r.uc;
-          vc = (float)r.vc;
-          px = (float)r.px;
-          py = (float)r.py;
+          o = ykf::v3{r.ox, r.oy, r.oz};
+          d = ykf::v3{r.dx, r.dy, r.dz};
         }
       }
       if (!pre) {
+        const bool lens = ka.cam.lens_radius > 0;  // (decided in double, as for the warm-up)
         rng_start_full(g, seed);
-        uc = f_uniform01(g);
-        vc = f_uniform01(g);
+        const float uc = f_uniform01(g);
+        const float vc = f_uniform01(g);
+        float px = 0, py = 0;
         if (lens) {  // thin-lens extension: random_in_unit_disk by rejection, x then y
           do {
             px = ykf::uniform(g, -1.0f, 1.0f);
             py = ykf::uniform(g, -1.0f, 1.0f);
           } while (!(px * px + py * py < 1.0f));
         }
-      }
-      // (x + U01) / W with x, W unsigned → float (uniform_real_distribution<float>)
-      const float u = ((float)x + uc) / ka.camf.w;
-      const float v = ((float)(ka.H - y - 1) + vc) / ka.camf.h;
-      const ykf::v3 cam_o = ykf::off(ka.camf.origin), cam_llc = ykf::off(ka.camf.llc);
-      const ykf::v3 cam_h = ykf::off(ka.camf.horizontal), cam_v = ykf::off(ka.camf.vertical);
-      d = ykf::sub(ykf::add(ykf::add(cam_llc, ykf::mul(cam_h, u)), ykf::mul(cam_v, v)), cam_o);
-      o = cam_o;
-      if (lens) {
-        const float lr = ka.camf.lens_radius;
-        const float rx = px * lr, ry = py * lr;
-        const ykf::v3 off = ykf::add(ykf::mul(ykf::off(ka.camf.lens_u), rx), ykf::mul(ykf::off(ka.camf.lens_v), ry));
-        o = ykf::add(o, off);
-        d = ykf::sub(d, off);
+        camera_ray_f32(ka.camf, ka.H, x, y, uc, vc, lens, px, py, o, d);
       }
       depth = ka.max_depth;
       nstk = 0;
@@ -1643,7 +1673,7 @@ struct ykgpu_context {
   int cus = 0;
   DevTree t64, t32;  // the FP64 and FP32 kernels' trees over the current scene
   size_t scratch_lanes = 0;
-  char* d_warm = nullptr;  // warm-up ring: StartRec (FP64 mt19937) or x_397 (FP32) per sample slot
+  char* d_warm = nullptr;  // warm-up ring: a StartRec (FP64) or StartRecF (FP32) per sample slot
   double* d_col = nullptr;     // sample colours of one launch (kColStride doubles per slot)
   double* d_acc = nullptr;     // running per-pixel sums between launches
   size_t col_cap = 0, acc_cap = 0;
@@ -1759,8 +1789,8 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, size_t lanes, bool ne
 #endif
 constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colours per launch at most
 // a launch's slots are bounded by the colour budget (kmax in launch()), and the render kernel
-// addresses a slot's StartRec as 3 * slot uint4s in 32-bit arithmetic
-static_assert(kColourBytes / (8 * kColStride) * 3 < (1ull << 32), "3 * slot must fit 32 bits");
+// addresses a slot's start record as 4 * slot uint4s (FP32: 3) in 32-bit arithmetic
+static_assert(kColourBytes / (8 * kColStride) * 4 < (1ull << 32), "4 * slot must fit 32 bits");
 // samples per pixel per launch at most: many mid-sized launches beat a few big ones, because the
 // launches alternate between two streams and each one's drain overlaps the next one's start
 // (round 1, 1920x1080x512 259.5 -> 254.0 ms at 64 spp/launch; with the render
@@ -1777,11 +1807,11 @@ constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
 #define YK_LAUNCH_SLOTS (1u << 25)
 #endif
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
-// x_397 buffers: the warm-ups run on ctx->aux, beside the render launches (their wave slots and
-// VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots idle), into
-// a ring of min(launches, kWarmBytes / slot) slots, at least 3; warm-up c waits for the render of
-// launch c - ring.  With the whole call in the ring (1920x1080x512: 4.25 GB) every warm-up is
-// queued at once and none waits for a render to end.
+// Start-record buffers: the warm-ups run on ctx->aux, beside the render launches (their wave
+// slots and VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots
+// idle), into a ring of min(launches, kWarmBytes / launch) launches, at least 3; warm-up c waits
+// for the render of launch c - ring.  (A 32-spp launch of 1920x1080 holds 4.2 GB of FP64 records:
+// the ring keeps 3, and a warm-up runs at most two launches ahead.)
 constexpr uint64_t kWarmBytes = 8ull << 30;
 #ifndef YK_FIRST_LAUNCH
 #define YK_FIRST_LAUNCH 8
@@ -1873,7 +1903,7 @@ uint32_t warm_per_cu(bool f32) {
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
   const bool f32 = p->precision == YK_PRECISION_FP32;
-  const bool x128 = p->rng == YK_RNG_XOR128;  // no x_397 warm-ups, no MT scratch
+  const bool x128 = p->rng == YK_RNG_XOR128;  // no warm-ups, no MT scratch
   const DevTree& tree = f32 ? ctx->t32 : ctx->t64;
   const DevTree::Plan& plan = tree.plan[x128 ? 1 : 0];
   const int grid = plan.grid, block = block_of(x128);
@@ -1937,8 +1967,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     return YK_OK;
   };
   const uint32_t nlaunch = (uint32_t)sched.size();
-  // warm-up records: the FP64 kernel's whole sample start (StartRec), the FP32 kernel's x_397
-  const size_t welem = sizeof(StartRec);  // per sample slot
+  // warm-up records: each sample's whole start (StartRec, FP32 StartRecF)
+  const size_t welem = f32 ? sizeof(StartRecF) : sizeof(StartRec);  // per sample slot
   const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (welem * nps * K)));
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
@@ -2019,7 +2049,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.band_log2 = p->row_band_log2;
   wa.out = ctx->d_warm;
   wa.lens = ctx->cam.lens_radius > 0 ? 1u : 0u;
-  wa.pad_w = 0;
+  wa.H = p->image_height;
+  wa.cam = ctx->cam;
+  wa.camf = ka.camf;
+  wa.w_d = ka.w_d;
+  wa.h_d = ka.h_d;
+  wa.inv_w = ka.inv_w;
+  wa.inv_h = ka.inv_h;
   wa.npix_slots = nps;
   fastdiv(nps, wa.nps_m, wa.nps_sh);
   fastdiv(p->image_width, wa.w_m, wa.w_sh);
@@ -2101,13 +2137,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
     ka.start = (const void*)wring;
     // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
-    // only on its own x_397 and colour buffer, so its blocks take the CUs that launch c's
+    // only on its own start records and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
     const hipStream_t rs = (c & 1) ? ctx->alt : ctx->ren;
     const size_t lanes = (size_t)grid * block;
     ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (c & 1) * lanes * ykd::kMtN : nullptr;
     ka.id_scratch = ctx->d_ids + (c & 1) * lanes * ctx->id_stride;
-    YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its x_397
+    YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its start records
     if (c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
     ka.pixel_counter = ctx->d_counter + c;
     YK_HIP(hipEventRecord(ev[2], rs));
