@@ -78,6 +78,14 @@ __device__ __forceinline__ v3 divs_fast(v3 a, double s) {
   if (__builtin_expect(__ballot(!ok) != 0, 0)) q = divs(a, s);
   return q;
 }
+// the same with the divisor's refined reciprocal r = rcp_refined(s) computed beforehand (the hit
+// normal's division by the radius: yk_mat_prep computes it once per sphere)
+__device__ __forceinline__ v3 divs_fast_r(v3 a, double s, double r) {
+  v3 q = {div_by(a.x, s, r), div_by(a.y, s, r), div_by(a.z, s, r)};
+  const bool ok = div_range(s) && num_range(a.x) && num_range(a.y) && num_range(a.z);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) q = divs(a, s);
+  return q;
+}
 // n / d for n >= 0 and a small integer d with y = RN(1/d) from the host: Markstein's theorem
 // (y correctly rounded, q0 = RN(n*y) within an ulp => fma(fma(-d, q0, n), y, q0) = RN(n/d)).
 __device__ __forceinline__ double div_markstein(double n, double d, double y) {

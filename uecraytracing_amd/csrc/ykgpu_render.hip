@@ -73,7 +73,7 @@ struct alignas(16) SphereMat {
   double ar, ag, ab, fuzz;
   double radius, ior;
   uint32_t kind, pad0;
-  uint64_t pad1;
+  double inv_r;  // ykd::rcp_refined(radius), computed on the device by yk_mat_prep
 };
 static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
 
@@ -481,6 +481,14 @@ __device__ __forceinline__ void reduce_slot(const ReduceArgs& ra, uint32_t p) {
 __global__ __launch_bounds__(256) void yk_reduce_samples(ReduceArgs ra) {
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < ra.npix_slots; p += gridDim.x * blockDim.x)
     reduce_slot(ra, p);
+}
+
+// The refined reciprocal of every radius, by the same instructions the division sequence uses
+// (rcp_refined), so the hit normal's (p - c) / radius reuses it (divs_fast_r: bit-identical to
+// divs_fast).  Run once per set_scene.
+__global__ void yk_mat_prep(SphereMat* m, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) m[i].inv_r = ykd::rcp_refined(m[i].radius);
 }
 
 // ykgpu_math_div: the renderer's vector / scalar division (divs_fast) on a buffer (diagnostic).
@@ -925,7 +933,7 @@ void yk_render_persistent(KernelArgs ka) {
         m = mat[hid];
         // hit record (sphere.hpp:41-45, hittable.hpp:23-27)
         p = ykd::add(o, ykd::mul(d, T));
-        const v3 outward = ykd::divs_fast(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius);
+        const v3 outward = ykd::divs_fast_r(ykd::sub(p, v3{sg.cx, sg.cy, sg.cz}), m.radius, m.inv_r);
         front = ykd::dot(d, outward) < 0;
         nrm = front ? outward : ykd::neg(outward);
       }
@@ -2418,7 +2426,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
     // sphere<float>: centre and radius rounded to float, radius*radius a float product
     const float rf = (float)s.radius;
     geo_f[i] = make_float4((float)s.center[0], (float)s.center[1], (float)s.center[2], rf * rf);
-    mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0u, 0ull};
+    mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0u, 0.0};  // inv_r: yk_mat_prep
   }
   YK_HIP(hipSetDevice(ctx->device));
   // a render enqueued by ykgpu_render_async on the caller's stream (and its launches on the
@@ -2481,6 +2489,9 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   // scale renders FP32 with the linear scan throughout
   if (!(rmin >= 0x1p-20) || !(ctx->t32.origin_bound <= 0x1p20)) ctx->t32.origin_bound = -1.0;
   YK_HIP(hipMemcpy(ctx->d_mat, mat.data(), count * sizeof(SphereMat), hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(yk_mat_prep, dim3((count + 255) / 256), dim3(256), 0, ctx->stream, ctx->d_mat, count);
+  YK_HIP(hipGetLastError());
+  YK_HIP(hipStreamSynchronize(ctx->stream));
   ctx->nspheres = count;
   ctx->cam = *camera;
   ctx->have_scene = true;
