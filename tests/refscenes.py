@@ -84,3 +84,27 @@ def graze():
         metal((0.4, -0.1, -1.5), 0.1, (0.9, 0.8, 0.7)),
         lambertian((-0.4, -0.0999, -1.2), 0.1, (0.2, 0.8, 0.3)),
     ]
+
+
+def axial():
+    """Slow-axis stress for the FP32 cone: a lattice of small spheres strung
+    along -z in front of a narrow-field camera (axial_camera), so first-segment rays run within
+    a few cone slopes of the z axis on x and y at once, over a ground sphere."""
+    s = [lambertian((0, -1000.0, -10), 999.7, (0.5, 0.5, 0.5))]
+    for i, z in enumerate(range(-2, -42, -3)):
+        for j, (x, y) in enumerate(((-0.12, 0.5), (0.0, 0.46), (0.12, 0.55), (0.0, 0.62), (0.05, 0.5))):
+            r = 0.02 + 0.01 * ((i + j) % 3)
+            if (i + j) % 4 == 0:
+                s.append(metal((x, y, float(z)), r, (0.8, 0.7, 0.6), 0.1 * ((i + j) % 2)))
+            else:
+                s.append(lambertian((x, y, float(z)), r, (0.3 + 0.05 * j, 0.6, 0.2 + 0.05 * i)))
+    return s
+
+
+def axial_camera() -> Camera:
+    """A pinhole at (0, 0.5, 0) looking down -z through a 0.02 x 0.01 window at distance 1: every
+    camera ray has |d_x| <= 0.01 and |d_y| <= 0.005 against |d_z| = 1."""
+    h, v = (0.02, 0.0, 0.0), (0.0, 0.01, 0.0)
+    o = (0.0, 0.5, 0.0)
+    llc = tuple(((o[i] - h[i] / 2) - v[i] / 2) - (0.0, 0.0, 1.0)[i] for i in range(3))
+    return Camera(D3(*o), D3(*llc), D3(*h), D3(*v), D3(0, 0, 0), D3(0, 0, 0), 0.0)

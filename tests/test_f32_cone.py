@@ -12,6 +12,8 @@ the origin bound as the FP32 tree grows them, and checks: every box the exact co
 Test infrastructure only (numpy model of device arithmetic)."""
 import numpy as np
 
+import refscenes
+
 KCONE = np.float32(2.0 ** -8 * (1 + 2.0 ** -10))
 FAR_AT = np.float32(1 + 2.0 ** -10)
 SLOW_AT = np.float32(1 - 2.0 ** -10)
@@ -139,3 +141,23 @@ def test_slow_axis_bound_culls():
     culled = (without & ~with_l)[slow].sum()
     kept = without[slow].sum()
     assert culled > 0.2 * kept, (culled, kept)  # and for slow rays it removes many
+
+
+def test_axial_scene_exercises_slow_axes():
+    """The axial camera's rays are slow on x and y (|d_k| < kF32Cone |d|) for most
+    pixels: the FP32 tree's slow-axis bound and its two-slow-axes case are really exercised."""
+    cam = refscenes.axial_camera()
+    k = 2.0 ** -8 * (1 + 2.0 ** -10)
+    slow_x = slow_y = both = 0
+    n = 0
+    for u in np.linspace(0, 1, 41):
+        for v in np.linspace(0, 1, 21):
+            d = [cam.lower_left_corner[i] + u * cam.horizontal[i] + v * cam.vertical[i] - cam.origin[i] for i in range(3)]
+            s = k * float(np.sqrt(sum(x * x for x in d)))
+            sx, sy = abs(d[0]) < s, abs(d[1]) < s
+            slow_x += sx
+            slow_y += sy
+            both += sx and sy
+            n += 1
+    assert slow_y > 0.5 * n and slow_x > 0.2 * n and both > 0.1 * n
+

@@ -107,6 +107,8 @@ def test_fp32_row_tiles_and_counts(ren):
 def _scene(name, seed):
     if name in refscenes.SCENES:
         return refscenes.SCENES[name](), refscenes.reference_camera()
+    if name == "axial":
+        return refscenes.axial(), refscenes.axial_camera()
     if name in ("dupes", "graze"):
         return getattr(refscenes, name)(), refscenes.reference_camera()
     if name == "large":
@@ -128,7 +130,7 @@ def _scene(name, seed):
 
 
 FP32_TREE = [("final", 42), ("glass", 3), ("rtiow5", 0), ("mixed12", 0), ("dupes", 0), ("graze", 0),
-             ("large", 0)]
+             ("axial", 0), ("large", 0)]
 
 
 @pytest.mark.parametrize("name,seed", FP32_TREE, ids=[f"{n}-{s}" for n, s in FP32_TREE])
@@ -151,7 +153,7 @@ def test_fp32_tree_matches_linear_scan_and_oracle(ren, name, seed):
         assert st["sphere_tests"] * 2 < st["segments"] * len(arr)
 
 
-@pytest.mark.parametrize("name,seed,W,spp", [("final", 42, 1920, 16), ("graze", 0, 960, 32)])
+@pytest.mark.parametrize("name,seed,W,spp", [("final", 42, 1920, 16), ("graze", 0, 960, 32), ("axial", 0, 480, 32)])
 def test_fp32_tree_whole_frame_equals_linear_scan(ren, name, seed, W, spp):
     """Whole frames in float (33 M and 17 M samples): tree == linear scan, sums bit for bit."""
     arr, cam = _scene(name, seed)
@@ -222,3 +224,4 @@ def test_xor128_row_tiles_random_seed_and_counts(ren):
     got = ren.render_sums(p)
     _, want, _, _ = oracle_lib.render(arr, cam, p, want_rgb=False, want_sums=True)
     assert got.tobytes() == want.tobytes()
+

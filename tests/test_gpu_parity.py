@@ -267,10 +267,12 @@ def _dupes_scene():
     return s
 
 
-@pytest.mark.parametrize("name,seed", [("final", 42), ("glass", 3), ("mixed12", 0), ("dupes", 0)])
+@pytest.mark.parametrize("name,seed", [("final", 42), ("glass", 3), ("mixed12", 0), ("dupes", 0), ("axial", 0)])
 def test_bvh_matches_linear_scan_and_oracle(ren, name, seed):
     if name == "dupes":
         arr, cam = _dupes_scene(), refscenes.reference_camera()
+    elif name == "axial":  # rays within a few 2^-8 slopes of the z axis (the FP32 cone's slow axes)
+        arr, cam = refscenes.axial(), refscenes.axial_camera()
     elif name == "mixed12":
         arr, cam = refscenes.mixed12(), refscenes.reference_camera()
     else:
