@@ -21,6 +21,12 @@ struct PkFmaF32 {
   using T = double;  // two packed floats in a 64-bit register pair
   static __device__ void op(T& x, T a, T b) { asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(x) : "v"(a), "v"(b)); }
 };
+struct FmaMixF32 {  // the BVH slab FMA with a binary16 plane (yk_bvh.hpp HalfNode)
+  using T = float;
+  static __device__ void op(T& x, T a, T b) {
+    asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(x) : "v"(a), "v"(b));
+  }
+};
 struct FmaF64 {
   using T = double;
   static __device__ void op(T& x, T a, T b) { asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(x) : "v"(a), "v"(b)); }
@@ -301,6 +307,7 @@ int main(int argc, char** argv) {
   for (int wps : {1, 2, 4, 8}) {
     chip_rate<FmaF32>("fma_f32", 2, 1.0000001f, 0.5f, 1.0f, wps);
     chip_rate<PkFmaF32>("pk_fma_f32", 4, 1.0, 0.5, 1.0, wps);
+    chip_rate<FmaMixF32>("fma_mix_f32", 2, 1.0f, 0.5f, 1.0f, wps);
     chip_rate<FmaF64>("fma_f64", 2, 1.0000001, 0.5, 1.0, wps);
     chip_rate<MulLoU32>("mul_lo_u32", 0, 1812433253u, 0, 7u, wps);
     chip_rate<MadU64U32>("mad_u64_u32", 0, 1812433253u, 0, 7u, wps);
