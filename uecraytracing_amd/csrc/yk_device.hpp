@@ -178,14 +178,22 @@ constexpr uint32_t kMtN = 624, kMtM = 397, kLazyDraws = kMtN - kMtM;  // 227
 __device__ __forceinline__ uint32_t mt_seed_step(uint32_t prev, uint32_t i) {
   return 1812433253u * (prev ^ (prev >> 30)) + i;
 }
+// gfx950's three-input bitwise op (v_bitop3_b32: bit i of the result is bit
+// (a_i << 2 | b_i << 1 | c_i) of the table): a ^ (b & c) is table 0x78, (a & c) | (b & ~c) 0xE4
+__device__ __forceinline__ uint32_t xor_and(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x78);
+}
 __device__ __forceinline__ uint32_t mt_mix(uint32_t hi_src, uint32_t lo_src) {
-  const uint32_t y = (hi_src & 0x80000000u) | (lo_src & 0x7fffffffu);
-  return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  // y = upper bit of hi_src, lower 31 of lo_src; (y >> 1) ^ (y odd ? 0x9908b0df : 0), the
+  // odd test read from lo_src (y & 1 = lo_src & 1) as an all-ones / zero mask: 5 instructions
+  const uint32_t y = __builtin_amdgcn_bitop3_b32(hi_src, lo_src, 0x80000000u, 0xE4);
+  const uint32_t odd = 0u - (lo_src & 1u);
+  return xor_and(y >> 1, odd, 0x9908b0dfu);
 }
 __device__ __forceinline__ uint32_t mt_temper(uint32_t z) {  // random.hpp:98-102
   z ^= (z >> 11);
-  z ^= (z << 7) & 0x9d2c5680u;
-  z ^= (z << 15) & 0xefc60000u;
+  z = xor_and(z, z << 7, 0x9d2c5680u);   // z ^= (z << 7) & 0x9d2c5680
+  z = xor_and(z, z << 15, 0xefc60000u);  // z ^= (z << 15) & 0xefc60000
   z ^= (z >> 18);
   return z;
 }

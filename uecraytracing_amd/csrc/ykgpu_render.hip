@@ -825,6 +825,17 @@ void yk_render_persistent(KernelArgs ka) {
               }
               continue;
             }
+            // no slot entered: pop here, inside the visit branch, so the lane goes on with the
+            // popped node in the next trip instead of waiting for every other lane of the wave to
+            // stop descending (512 spp: 180.8 -> 178.4 ms); an empty stack ends the traversal as
+            // the empty leaf (~0: no spheres)
+            if (top == stk) {
+              node = ykbvh::kEmptyLeaf;
+            } else {
+              top -= kBlk;
+              node = *top;
+            }
+            continue;
           } else {
             YK_STAMP(2);  // interior nodes since the last stamp
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
@@ -1386,6 +1397,13 @@ void yk_render_f32(KernelArgs ka) {
               }
               continue;
             }
+            if (top == stk) {  // as in the FP64 kernel
+              node = ykbvh::kEmptyLeaf;
+            } else {
+              top -= kBlk;
+              node = *top;
+            }
+            continue;
           } else {
             YK_STAMP(2);
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
