@@ -366,9 +366,10 @@ template <bool kLazy = false, class G>
 __device__ __forceinline__ double canonical(G& g) {
   const double u0 = (double)rng_next<kLazy>(g);
   const double u1 = (double)rng_next<kLazy>(g);
-  double sum = u0;
-  sum = sum + u1 * 4294967296.0;
-  double r = sum / 18446744073709551616.0;
+  // RN(u0 + u1 2^32) / 2^64 as ONE fma of the exactly scaled terms, u1 2^-32 + u0 2^-64: both
+  // products are exact and a power-of-two scaling commutes with rounding in the normal range
+  // (every term is 0 or >= 2^-64), so the result is the reference's bit for bit
+  double r = __builtin_fma(u1, 0x1p-32, u0 * 0x1p-64);
   if (r >= 1.0) r = 1.0 - 0x1p-53;
   return r;
 }
@@ -378,7 +379,13 @@ __device__ __forceinline__ double uniform(G& g, double a, double b) {
   return (canonical<kLazy>(g) * (b - a)) + a;
 }
 // uniform_real_distribution::operator() on an already drawn canonical c: the same c*(b-a)+a
-__device__ __forceinline__ double uniform_of(double c, double a, double b) { return (c * (b - a)) + a; }
+// (Every call passes constant bounds.  (-1, 1): c*2 is exact, so c*2 + -1 is one fma with the same
+// rounding; (0, 1): c*1 + 0 is c, as c >= 0.)
+__device__ __forceinline__ double uniform_of(double c, double a, double b) {
+  if (a == -1.0 && b == 1.0) return __builtin_fma(c, 2.0, -1.0);
+  if (a == 0.0 && b == 1.0) return c;
+  return (c * (b - a)) + a;
+}
 // Whether the next two words may be drawn speculatively and then given back by restoring a copy
 // of the lane's engine: for mt19937 only inside the lazy cursors (the scratch engine's twist
 // rewrites its state in place); xor128's state is the copy.
