@@ -424,19 +424,9 @@ def main():
         t = time.perf_counter()
         oracle_lib.render_as_shipped(spheres, cam, ra, nthreads=nthreads)
         dta = time.perf_counter() - t
-        # and one thread per logical CPU of the node (the verdict's "node's count"): the job's
-        # cgroup quota, not the thread count, bounds it
-        tn = time.perf_counter()
-        oracle_lib.render(spheres, cam, ra, nthreads=node_cpus)
-        dtn = time.perf_counter() - tn
         result["cpu_baseline"]["variants"] = {
             "port_1_core": {"value": round(W * spp / dt1 / 1e6, 4), "cores": 1,
                             "sample": f"row {H // 2} x {W} px x {spp} spp, {dt1:.1f} s"},
-            "port_node_threads": {
-                "value": round(len(rows_as) * W * spp / dtn / 1e6, 4), "cores": node_cpus,
-                "sample": f"{len(rows_as)} rows (every {args.cpu_row_step * 4}th) x {W} px x {spp} spp, "
-                          f"{dtn:.1f} s; {node_cpus} threads = the node's logical CPUs, run under this "
-                          f"job's {quota} CPU quota"},
             "as_shipped_cost_model": {
                 "value": round(len(rows_as) * W * spp / dta / 1e6, 4), "cores": nthreads,
                 "sample": f"{len(rows_as)} rows (every {args.cpu_row_step * 4}th) x {W} px x {spp} spp, "
