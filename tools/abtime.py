@@ -2,7 +2,7 @@
 instance, flags=0): one subprocess per variant run (one library per process), interleaved.
 usage: python tools/abtime.py <spp> <variant> [<variant> ...]   (variant 'base' = lib/libykgpu.so,
 otherwise lib/abl/libykgpu_<variant>.so; "<variant>@VAR=value[@VAR2=value2...]" also sets
-environment variables of that run, e.g. base@YKGPU_BVH_LEAF_F32=1); AB_ROWS="begin:count:stride" renders a row tile only
+environment variables of that run, e.g. base@YKGPU_BVH_BINS=32); AB_ROWS="begin:count:stride" renders a row tile only
 (e.g. "0:135:8" = rank 0 of 8); AB_PREC=1 times the FP32 mode"""
 import json
 import os
