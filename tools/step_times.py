@@ -21,16 +21,24 @@ stream = torch.cuda.Stream()
 with torch.cuda.stream(stream):
     ren.render_async(p, tile.data_ptr(), stream.cuda_stream)
 torch.cuda.synchronize()
-ev = []
+import time  # noqa: E402
+ev, host, lib = [], [], []
 for _ in range(steps):
     with torch.cuda.stream(stream):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
+        t = time.perf_counter()
         ren.render_async(p, tile.data_ptr(), stream.cuda_stream)
+        host.append(round((time.perf_counter() - t) * 1e3, 2))
         b.record(stream)
         ev.append((a, b))
     if sync_each:
         torch.cuda.synchronize()
+        st = ren.stats()
+        lib.append((round(st["kernel_ms"], 1), round(st["render_busy_ms"], 1)))
 torch.cuda.synchronize()
 ts = [round(a.elapsed_time(b), 2) for a, b in ev]
 print("sync_each" if sync_each else "async", ts, "mean", round(sum(ts) / len(ts), 2), "min", min(ts))
+print("  host enqueue ms", host)
+if lib:
+    print("  library (kernel_ms, render_busy_ms)", lib)

@@ -2003,8 +2003,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const uint32_t nlaunch = (uint32_t)sched.size();
   // warm-up records: each sample's whole start (StartRec, FP32 StartRecF)
   const size_t welem = f32 ? sizeof(StartRecF) : sizeof(StartRec);  // per sample slot
-  const uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
+  uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
       nlaunch, std::max<uint64_t>(3, kWarmBytes / (welem * nps * K)));
+  if (const char* e = std::getenv("YKGPU_WARM_RING"))  // (A/B) launches of start records ahead
+    kWarmRing = (uint32_t)std::min<uint64_t>(nlaunch, (uint64_t)std::max(2, std::atoi(e)));
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
   // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
   // reduce c (stream red) overlaps the renders after it
