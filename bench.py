@@ -159,8 +159,8 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)  # single steps vary by up to ±3% (profiles/r03_ab/variance/): 8 steps ≈ 1.5 s
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--depth", type=int, default=50)
