@@ -150,9 +150,50 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf):
             "segments_per_sample": round(st["segments"] / max(1, st["samples"]), 4),
             "mt_fallback_samples": st["mt_fallbacks"],
             "device_bytes": tst["device_bytes"],
+            "call_bytes": tst["call_bytes"],
             "parity_vs_cpu": {"image_rows_compared": ys, "bytes_differing": int((gpu != cpu).sum()),
                               "max_abs_levels": int(np.abs(gpu.astype(int) - cpu.astype(int)).max())},
         }
+    return out
+
+
+def rank_tiles(ren, stream, seed0, frame_ms):
+    """The N-GPU bound on this GPU: every rank's row tile of the N-way
+    split rendered ALONE (best of two calls, HIP events on the bench stream), for config 3 at
+    N = 2, 4, 8 and config 4's eight 270-row tiles.  The slowest tile bounds the N-GPU step before
+    the gather; `speedup_bound` = the single-GPU call (frame_ms, config 3; one timed config-4
+    frame otherwise) / the slowest tile."""
+    import torch
+
+    import uecraytracing_amd as yk
+    from uecraytracing_amd.records import image_height_for, make_params
+    from uecraytracing_amd.tiles import tile_rows
+
+    def call_ms(p, out):
+        best = None
+        for _ in range(2):
+            with torch.cuda.stream(stream):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                ren.render_async(p, out.data_ptr(), stream.cuda_stream)
+                e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        return best
+
+    out = {}
+    for cfg, W, spp, ns in (("config3", 1920, 512, (2, 4, 8)), ("config4", 3840, 1024, (8,))):
+        spheres, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
+        ren.set_scene(spheres, cam)
+        H = image_height_for(W)
+        buf = torch.empty((H, W, 3), dtype=torch.uint8, device=torch.device("cuda", ren.device))
+        full = frame_ms if cfg == "config3" else call_ms(make_params(W, H, spp, 50, seed0, flags=0), buf)
+        for n in ns:
+            ms = [call_ms(make_params(W, H, spp, 50, seed0, rows=tile_rows(r, n, H), flags=0), buf) for r in range(n)]
+            out[f"{cfg}_n{n}"] = {"tile_ms": [round(m, 3) for m in ms], "slowest_ms": round(max(ms), 3),
+                                  "frame_ms": round(full, 3), "speedup_bound": round(full / max(ms), 3),
+                                  "slowest_over_ideal": round(max(ms) / (full / n), 4)}
     return out
 
 
@@ -176,6 +217,8 @@ def parse():
                     help="skip the one-call timings of the FP32 and xor128 modes (rank 0, N=1)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the BASELINE config 4 / 5 measurements (rank 0, N=1)")
+    ap.add_argument("--no-tiles", action="store_true",
+                    help="skip the per-rank tile timings of the N-GPU splits (rank 0, N=1)")
     return ap.parse_args()
 
 
@@ -364,11 +407,12 @@ def main():
                     "achieved": round(hbm_gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 7), "traffic": traffic,
                     "traffic_over_algorithmic": round(traffic / (hbm_step / launches), 1) if traffic else None,
-                    "device_bytes": tst["device_bytes"],
+                    "device_bytes": tst["device_bytes"], "call_bytes": tst["call_bytes"],
                     "algorithmic": f"SURVEY §8(d): the RGB8 image ({rows_mine * W * 3} B) once per "
                                    f"step + the scene ({scene_bytes} B) once per workgroup "
                                    f"({tst['grid_blocks']} per launch); traffic = PMC FETCH_SIZE x2 + "
-                                   f"WRITE_SIZE per launch (scratch: colours, x_397, MT state)"},
+                                   f"WRITE_SIZE per launch (scratch: the start records with the colours "
+                                   f"written over them, the processing order, MT fallback state)"},
             "checks": {"launches_x_launch_ms_le_step": bool(launches * launch_ms <= ms_per_step * 1.001)},
             # render = the launches' spans summed (they overlap); render_busy = their union
             "step_breakdown_ms": {"render_spans_summed": round(tst["kernel_ms"], 3),
@@ -461,6 +505,9 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_configs:
         result["configs"] = other_configs(ren, stream, args.seed0, args.cpu_threads or usable_cpus()[0], peak_tf)
+
+    if rank == 0 and world == 1 and not args.no_tiles and (W, spp, depth, args.scene) == (1920, 512, 50, "final"):
+        result["tiles"] = rank_tiles(ren, stream, args.seed0, call_ms)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -185,9 +185,19 @@ inline std::vector<int> devices_from_env(const char* var = "YKGPU_DEVICES") {
     d.push_back(k);
     i += used;
     if (i < v.size() && v[i] != ',') throw error(YK_ERR_INVALID, std::string(var) + ": not a device list: " + v);
-    if (i < v.size()) ++i;
+    if (i < v.size()) {
+      ++i;
+      if (i == v.size()) throw error(YK_ERR_INVALID, std::string(var) + ": trailing ',' in " + v);
+    }
   }
   if (d.empty()) throw error(YK_ERR_INVALID, std::string(var) + ": empty device list");
+  // every index must name a device of this node (before any context is created)
+  int n = 0;
+  check(ykgpu_device_count(&n), (std::string(var) + ": ykgpu_device_count").c_str());
+  for (int k : d)
+    if (k >= n)
+      throw error(YK_ERR_INVALID, std::string(var) + ": device " + std::to_string(k) + " of " + v + " does not exist (" +
+                                      std::to_string(n) + " devices)");
   return d;
 }
 
@@ -239,13 +249,19 @@ class renderer {
 
   std::vector<uint8_t> render(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
                               uint32_t seed0, const render_options& o) {
-    const yk_render_params p = params(width, height, spp, max_depth, seed0, o);
     std::vector<uint8_t> img((size_t)width * height * 3);
-    if (group_)
-      check(ykgpu_group_render(group_, &p, img.data()), "ykgpu_group_render");
-    else
-      check(ykgpu_render(ctx_, &p, img.data()), "ykgpu_render");
+    render_into(img.data(), width, height, spp, max_depth, seed0, o);
     return img;
+  }
+
+  // The same into the caller's W*H*3 bytes (the patched source.cpp's image_t, filled in place)
+  void render_into(uint8_t* rgb, uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,
+                   uint32_t seed0, const render_options& o = render_options{}) {
+    const yk_render_params p = params(width, height, spp, max_depth, seed0, o);
+    if (group_)
+      check(ykgpu_group_render(group_, &p, rgb), "ykgpu_group_render");
+    else
+      check(ykgpu_render(ctx_, &p, rgb), "ykgpu_render");
   }
 
   static yk_render_params params(uint32_t width, uint32_t height, uint32_t spp, uint32_t max_depth,

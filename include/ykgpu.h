@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 8u
+#define YKGPU_ABI_VERSION 9u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 (reflected + fuzz * the reference's random_in_unit_sphere,
@@ -178,8 +178,12 @@ typedef struct yk_render_stats {
                               shaded as [1] lambertian, [2] metal, [3] of them fuzzy,
                               [4] dielectric; [5..7] 0                                   */
   uint64_t device_bytes;   /* device memory the context holds after the call: scene, BVHs,
-                              processing order, warm-up and colour rings, running sums, MT
-                              and attenuation scratch, output buffers      */
+                              processing order, start-record (xor128: colour) ring, running
+                              sums, MT and attenuation scratch, output buffers.
+                              Buffers follow the calls: grown when a call needs more, given
+                              back when it needs less than half                            */
+  uint64_t call_bytes;     /* device memory THIS call needed (the same items sized to it):
+                              1920x1080x512 FP64 ~13.7 GB; a 270-row tile of 3840 ~7.4 GB   */
 } yk_render_stats;
 
 typedef struct ykgpu_context ykgpu_context;

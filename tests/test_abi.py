@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = yk.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 8
+    assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 9
 
 
 def test_reference_camera_matches_camera_hpp():
@@ -103,9 +103,11 @@ def test_group_invalid_arguments_are_reported():
 
 
 def test_render_stats_layout_matches_the_header():
-    """yk_render_stats ends with device_bytes at offset 312 (include/ykgpu.h, ABI 8)."""
+    """yk_render_stats ends with device_bytes at offset 312 and call_bytes at 320 (include/ykgpu.h,
+    ABI 9)."""
     assert records.RenderStats.device_bytes.offset == 312
-    assert ctypes.sizeof(records.RenderStats) == 320
+    assert records.RenderStats.call_bytes.offset == 320
+    assert ctypes.sizeof(records.RenderStats) == 328
 
 
 def test_invalid_arguments_are_reported():

@@ -18,7 +18,7 @@ CLI = yk.CLI_PATH
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_BIN = os.path.join(ROOT, "oracle", "_ref")
 DROPIN = os.path.join(REF_BIN, "ref_dropin")
-PATCHED = {k: os.path.join(REF_BIN, "raytrace_ykgpu" + k) for k in ("", "_16x2", "_200x8")}
+PATCHED = {k: os.path.join(REF_BIN, "raytrace_ykgpu" + k) for k in ("", "_16x2", "_200x8", "_3840x2")}
 CX16 = os.path.join(REF_BIN, "raytrace_cx16")
 RT16 = os.path.join(REF_BIN, "raytrace_rt16")
 MAN = golden_data.manifest()
@@ -202,10 +202,34 @@ def test_patched_reference_on_several_devices(tmp_path):
     assert a.returncode == b.returncode == 0 and a.stdout == b.stdout
 
 
+@pytest.mark.gpu
+def test_patched_reference_at_config4_geometry_on_eight_contexts(tmp_path):
+    """Config 4's image size through the reference's own main, cxxopts and stb: 3840x2160 (the
+    size whose 24.9 MB image_t overflows the unmodified runtime build's 8 MB stack) at
+    2 spp, its rows dealt over eight contexts (YKGPU_DEVICES=0,...,0: the 8-GPU split's 270-row
+    tiles), run under the default 8 MB stack; rows 0, 1079 and 2159 equal the oracle's."""
+    need(PATCHED["_3840x2"])
+    env = dict(os.environ, YKGPU_DEVICES=",".join(["0"] * 8))
+    r = subprocess.run(["bash", "-c", 'ulimit -s 8192 && "$0" "$1"', PATCHED["_3840x2"], "c4.png"],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.splitlines() == ["rendering...", "rendering finished", "write to file : c4.png", "success"]
+    rgb, W, H = golden_data.png_rgb(str(tmp_path / "c4.png"))
+    assert (W, H) == (3840, 2160)
+    img = np.frombuffer(rgb, np.uint8).reshape(H, W, 3)
+    import oracle_lib
+    import refscenes
+    for rows in ((0, 2, 2159), (1079, 1, 1)):
+        want, _, _, _ = oracle_lib.render(refscenes.ref4(), refscenes.reference_camera(),
+                                          yk.make_params(3840, 2160, 2, 50, 404, rows=rows), nthreads=16)
+        ys = [rows[0] + k * rows[2] for k in range(rows[1])]
+        np.testing.assert_array_equal(img[ys], want)
+
+
 def test_patched_reference_rejects_a_bad_device_list(tmp_path):
     """YKGPU_DEVICES that is not a device list fails loudly before any device is touched."""
     need(PATCHED["_16x2"])
-    for bad in ("x", "0,,1", "-1", "0;1"):
+    for bad in ("x", "0,,1", "-1", "0;1", "0,", "99"):
         r = subprocess.run([PATCHED["_16x2"], "o.png"], cwd=tmp_path, capture_output=True, text=True, timeout=300,
                            env=dict(os.environ, YKGPU_DEVICES=bad))
         assert r.returncode != 0

@@ -45,6 +45,7 @@ def test_group_equals_the_reference_golden(entries):
         for e, s in enumerate(per):
             assert s["samples"] == len(tile_image_rows(e, entries, 112)) * 200 * 8
         assert tot["device_bytes"] >= sum(s["device_bytes"] for s in per) > 0
+        assert tot["call_bytes"] >= sum(s["call_bytes"] for s in per) > 0
 
 
 def test_group_final_scene_strided_rows_equal_single(single):

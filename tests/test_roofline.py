@@ -98,3 +98,10 @@ def test_rocprof_union_agrees_with_bench_launch_ms():
     b = json.load(open(bench))
     u = json.load(open(union))
     assert abs(u["union_per_dispatch_ms"] - b["roofline"]["launch_ms"]) / b["roofline"]["launch_ms"] < 0.05
+
+
+def test_peak_falls_back_to_the_datasheet_without_the_ubench_file(tmp_path):
+    """No ubench evidence (a tree without profiles/): the datasheet figure, said so."""
+    peak, ev = flops.fp64_valu_peak(str(tmp_path / "absent.jsonl"))
+    assert peak == flops.SPEC_FP64_VALU_TFLOPS
+    assert "datasheet" in ev["source"] and "absent" in ev["note"]

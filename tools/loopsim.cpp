@@ -424,6 +424,124 @@ int main(int argc, char** argv) {
     for (int q = 0; q < 16; ++q) printf(" [%d]%zu", q, ins_hist[q]);
     printf("\n");
   }
+  // ---- round 4: two traversals per lane (rays k and k + 64 of a 128-ray wave, each the ifelse
+  // loop; one trip issues both rays' blocks) and a two-node frontier of ONE ray per lane (the
+  // current node and, when it is an inner node, the stack top's inner node visited in the same
+  // trip; the last entered child of the pair is next, the rest pushed)
+  {
+    double trips = 0, vb = 0, lb = 0, lv = 0, ll = 0, rounds = 0;
+    size_t nw = 0;
+    std::vector<size_t> sthist(20, 0);
+    for (size_t g = 0; g + 128 <= idx.size(); g += 128, ++nw) {
+      std::vector<Lane> lanes(128);
+      for (int k = 0; k < 128; ++k) {
+        Lane& L = lanes[k];
+        L.o = seg[idx[g + k]].first;
+        L.d = seg[idx[g + k]].second;
+        L.a = dot(L.d, L.d);
+        L.ix = rcp((float)L.d.x), L.iy = rcp((float)L.d.y), L.iz = rcp((float)L.d.z);
+        L.node = M.root;
+      }
+      for (;;) {
+        bool act = false, v[2] = {false, false}, l[2] = {false, false};
+        for (int k = 0; k < 128; ++k) {
+          Lane& L = lanes[k];
+          if (L.done) continue;
+          act = true;
+          if (L.node >= 0) {
+            v[k >> 6] = true, ++lv;
+            M.visit(L);
+            if (L.node == kDone) L.done = true;
+          } else {
+            l[k >> 6] = true;
+            ll += M.leaf(L, L.node).first;
+            M.pop(L);
+            if (L.node == kDone) L.done = true;
+          }
+        }
+        for (auto& L : lanes) L.pend = std::max<int32_t>(L.pend, (int32_t)L.stk.size());
+        if (!act) break;
+        trips += 1;
+        vb += v[0] + v[1];
+        lb += l[0] + l[1];
+      }
+      for (auto& L : lanes) sthist[std::min<int32_t>(L.pend, 19)]++;
+    }
+    printf("stack depth (max per ray):");
+    for (int q = 0; q < 20; ++q) if (sthist[q]) printf(" [%d]%zu", q, sthist[q]);
+    printf("\n");
+    printf("2 rays/lane (128/wave)  per wave-trip-of-2-segments: trips %.1f, visit blocks %.1f, leaf blocks %.1f | "
+           "per ray: visits %.2f leaf tests %.2f\n",
+           trips / nw, vb / nw, lb / nw, lv / (128.0 * nw), ll / (128.0 * nw));
+    (void)rounds;
+  }
+  {
+    double trips = 0, vb = 0, vb2 = 0, lb = 0, lv = 0, ll = 0;
+    size_t nw = 0, maxst = 0;
+    for (size_t g = 0; g + 64 <= idx.size(); g += 64, ++nw) {
+      std::vector<Lane> lanes(64);
+      for (int k = 0; k < 64; ++k) {
+        Lane& L = lanes[k];
+        L.o = seg[idx[g + k]].first;
+        L.d = seg[idx[g + k]].second;
+        L.a = dot(L.d, L.d);
+        L.ix = rcp((float)L.d.x), L.iy = rcp((float)L.d.y), L.iz = rcp((float)L.d.z);
+        L.node = M.root;
+      }
+      for (;;) {
+        bool act = false, v = false, v2 = false, l = false;
+        for (auto& L : lanes) {
+          if (L.done) continue;
+          act = true;
+          if (L.node >= 0) {
+            v = true, ++lv;
+            int32_t second = kDone;
+            if (!L.stk.empty() && L.stk.back() >= 0) {
+              second = L.stk.back();
+              L.stk.pop_back();
+            }
+            // visit the first: its entered children (stack pushes + next)
+            Lane A = L;
+            A.stk.clear();
+            M.visit(A);  // A.node: next or kDone (after an empty pop of an empty stack)
+            std::vector<int32_t> ch(A.stk);
+            if (A.node != kDone) ch.push_back(A.node);
+            if (second != kDone) {
+              v2 = true, ++lv;
+              Lane B = L;
+              B.stk.clear();
+              B.node = second;
+              M.visit(B);
+              for (int32_t c2 : B.stk) ch.push_back(c2);
+              if (B.node != kDone) ch.push_back(B.node);
+            }
+            if (ch.empty()) {
+              M.pop(L);
+            } else {
+              L.node = ch.back();
+              ch.pop_back();
+              for (int32_t c2 : ch) L.stk.push_back(c2);
+            }
+            maxst = std::max(maxst, L.stk.size());
+            if (L.node == kDone) L.done = true;
+          } else {
+            l = true;
+            ll += M.leaf(L, L.node).first;
+            M.pop(L);
+            if (L.node == kDone) L.done = true;
+          }
+        }
+        if (!act) break;
+        trips += 1;
+        vb += v;
+        vb2 += v2;
+        lb += l;
+      }
+    }
+    printf("frontier-2              per wave-segment: trips %.1f, visit blocks %.1f (second visits %.1f), leaf blocks %.1f | "
+           "per lane: visits %.2f leaf tests %.2f | max stack %zu\n",
+           trips / nw, vb / nw, vb2 / nw, lb / nw, lv / (64.0 * nw), ll / (64.0 * nw), maxst);
+  }
   for (int variant = 0; variant < 4; ++variant) {
     double trips = 0, wv = 0, wl = 0, wd2 = 0, lv = 0, ll = 0, cost = 0;
     size_t nw = 0;

@@ -108,6 +108,11 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #endif
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
+// Spheres per BVH leaf the kernels' leaf code handles: the FP64 leaf test is loop-free for one
+// sphere, the FP32 leaf loop is unrolled for two.  ykgpu_set_scene builds the trees with these
+// as ykbvh::Options::max_leaf and upload_tree rejects a tree with a larger leaf (its extra spheres
+// would be skipped silently).
+constexpr uint32_t kLeafCapF64 = 1, kLeafCapF32 = 2;
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
 
 #ifndef YK_CLAIM
@@ -152,7 +157,7 @@ struct KernelArgs {
   const SphereGeo* __restrict__ geo;
   const SphereMat* __restrict__ mat;
   const float4* __restrict__ geo_f;  // FP32 path: (cx, cy, cz, r*r) rounded to float, tuple order
-  double* col;                       // sample colours: kColStride doubles per slot (colour_store)
+  double* col;                       // sample colours: a record per slot (colour_store)
   uint32_t* pixel_counter;           // sample-slot counter
   uint32_t* mt_scratch;
   uint16_t* id_scratch;
@@ -429,12 +434,16 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 // into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
 
-// A sample's colour record: r, g, b as one aligned 32-byte record per sample slot (one 16-byte
-// and one 8-byte store, the whole record in one 32-byte sector).  yk_reduce_samples reads the
-// records of consecutive slots, coalesced.
-constexpr size_t kColStride = 4;
+// A sample's colour record: r, g, b (one 16-byte and one 8-byte store) at the start of a
+// kStride-double record per sample slot.  The mt19937 kernels write it over the slot's own
+// StartRec (64 B; FP32: StartRecF, 48 B): the lane read the whole record when the path started,
+// so a launch needs no colour buffer of its own; xor128 launches, which have no
+// start records, write 32-byte records into a colour ring.  yk_reduce_samples reads the records
+// of consecutive slots.
+constexpr size_t kColStride = 4;  // xor128's colour records (doubles)
+template <size_t kStride>
 __device__ __forceinline__ void colour_store(double* col, uint32_t slot, double r, double g, double b) {
-  double* rec = col + (size_t)slot * kColStride;
+  double* rec = col + (size_t)slot * kStride;
   *(double2*)rec = make_double2(r, g);
   rec[2] = b;
 }
@@ -444,13 +453,13 @@ __device__ __forceinline__ void colour_store(double* col, uint32_t slot, double 
 // the last launch, to_color3b (source.cpp:73-83): /spp, math::sqrt, clamp [0, .999], *256,
 // truncate.  One thread per processing slot, coalesced over the SoA colours.
 struct ReduceArgs {
-  const double* col;  // col[(s_local * npix_slots + p) * kColStride + c]
+  const double* col;  // col[(s_local * npix_slots + p) * cstride + c]
   double* acc;        // running sums, acc[c * npix_slots + p]
   const uint32_t* order;
   uint8_t* rgb;
   double* sums;
   uint32_t npix_slots, nsl, ks, spp;
-  uint32_t first, last, pad0, pad1;
+  uint32_t first, last, cstride, pad1;  // cstride: doubles per colour record
 };
 __device__ __forceinline__ void reduce_slot(const ReduceArgs& ra, uint32_t p) {
   const uint32_t q = ra.order[p];
@@ -461,7 +470,7 @@ __device__ __forceinline__ void reduce_slot(const ReduceArgs& ra, uint32_t p) {
   for (uint32_t k = 0; k < ra.ks; ++k) {
     const size_t i = (size_t)k * ra.npix_slots + p;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[i * kColStride + c];
+    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[i * ra.cstride + c];
   }
   if (!ra.last) {
 #pragma unroll
@@ -842,6 +851,7 @@ void yk_render_persistent(KernelArgs ka) {
             // the FP64 tree has one sphere per leaf (max_leaf = 1: the builder's median fallback
             // never leaves more), so a leaf is tested without a loop (512 spp: -0.9%); the empty
             // leaf ~0 (cnt 0) tests nothing.  (`continue` inside the do-while(0) leaves the test.)
+            static_assert(kLeafCapF64 == 1, "the FP64 leaf test handles one sphere");
             if (cnt != 0) do {
               const uint32_t k = 0;
               const SphereGeo sg = leaf_geo[first + k];
@@ -1071,8 +1081,10 @@ void yk_render_persistent(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
-      // the sample's colour; yk_reduce_samples adds them in sample order
-      colour_store(ka.col, slot, L_r, L_g, L_b);
+      // the sample's colour (over its StartRec for mt19937); yk_reduce_samples adds them in
+      // sample order
+      colour_store<std::is_same<Gen, ykd::MtLane>::value ? sizeof(StartRec) / 8 : kColStride>(ka.col, slot, L_r,
+                                                                                             L_g, L_b);
       in_path = false;
     }
     YK_STAMP(5);
@@ -1417,7 +1429,7 @@ void yk_render_f32(KernelArgs ka) {
             // (the FP32 tree has at most two spheres per leaf: the loop unrolled, without a loop
             // counter or latch; FP32 512 spp: -2.7%)
 #pragma unroll
-            for (uint32_t k = 0; k < 2u; ++k) {
+            for (uint32_t k = 0; k < kLeafCapF32; ++k) {
               if (k >= cnt) break;
               const float4 sg = leaf_geo[first + k];
               const uint32_t id = leaf_ids[first + k];
@@ -1634,7 +1646,7 @@ void yk_render_f32(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
-      colour_store(ka.col, slot, L_r, L_g, L_b);
+      colour_store<kRec ? sizeof(StartRecF) / 8 : kColStride>(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
     YK_STAMP(5);
@@ -1818,13 +1830,15 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, size_t lanes, bool ne
   return YK_OK;
 }
 
-#ifndef YK_COLOUR_MB
-#define YK_COLOUR_MB 8192
+#ifndef YK_LAUNCH_MB
+#define YK_LAUNCH_MB 8192
 #endif
-constexpr uint64_t kColourBytes = (uint64_t)YK_COLOUR_MB << 20;  // sample colours per launch at most
-// a launch's slots are bounded by the colour budget (kmax in launch()), and the render kernel
-// addresses a slot's start record as 4 * slot uint4s (FP32: 3) in 32-bit arithmetic
-static_assert(kColourBytes / (8 * kColStride) * 4 < (1ull << 32), "4 * slot must fit 32 bits");
+// per-slot records of one launch (start records, which the colours overwrite; xor128: colours)
+// at most: bounds a launch's slots for very large tiles (kmax in launch())
+constexpr uint64_t kLaunchBytes = (uint64_t)YK_LAUNCH_MB << 20;
+// the render kernel addresses a slot's start record as 4 * slot uint4s (FP32: 3) in 32-bit
+// arithmetic: the smallest record (xor128's 32-byte colours) bounds the slot count
+static_assert(kLaunchBytes / (8 * kColStride) * 4 < (1ull << 32), "4 * slot must fit 32 bits");
 // samples per pixel per launch at most: many mid-sized launches beat a few big ones, because the
 // launches alternate between two streams and each one's drain overlaps the next one's start
 // (round 1, 1920x1080x512 259.5 -> 254.0 ms at 64 spp/launch; with the render
@@ -1841,12 +1855,16 @@ constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
 #define YK_LAUNCH_SLOTS (1u << 25)
 #endif
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
-// Start-record buffers: the warm-ups run on ctx->aux, beside the render launches (their wave
-// slots and VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots
-// idle), into a ring of min(launches, kWarmBytes / launch) launches, at least 3; warm-up c waits
-// for the render of launch c - ring.  (A 32-spp launch of 1920x1080 holds 4.2 GB of FP64 records:
-// the ring keeps 3, and a warm-up runs at most two launches ahead.)
-constexpr uint64_t kWarmBytes = 8ull << 30;
+// Start-record ring: the warm-ups run on ctx->aux, beside the render launches (their wave slots
+// and VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots idle),
+// into a ring of min(launches, kWarmRingDepth) launch buffers (YKGPU_WARM_RING overrides).  The
+// render writes each sample's colour over its start record and the reduce reads it there, so
+// warm-up c waits for the REDUCE of launch c - ring.  Sized to the call: ring x slots x record
+// (1920x1080 at 32 spp per launch: 66M slots x 64 B = 4.2 GB per launch buffer).
+#ifndef YK_WARM_RING
+#define YK_WARM_RING 3
+#endif
+constexpr uint32_t kWarmRingDepth = YK_WARM_RING;
 #ifndef YK_FIRST_LAUNCH
 #define YK_FIRST_LAUNCH 8
 #endif
@@ -1905,11 +1923,10 @@ hipError_t create_render_stream(hipStream_t* s) {
   return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
-// Colour buffers in flight (YKGPU_COL_RING overrides): up to 4, within kColRingBytes
-constexpr uint64_t kColRingBytes = 24ull << 30;
-uint32_t col_ring(uint32_t nps, uint32_t K) {
-  const uint64_t one = 8ull * kColStride * nps * K;
-  uint32_t r = (uint32_t)std::max<uint64_t>(2, std::min<uint64_t>(4, kColRingBytes / std::max<uint64_t>(1, one)));
+// xor128 colour buffers in flight (YKGPU_COL_RING overrides): 3 (the mt19937 kernels write their
+// colours into the start-record ring instead)
+uint32_t col_ring() {
+  uint32_t r = 3;
   if (const char* e = std::getenv("YKGPU_COL_RING")) r = (uint32_t)std::max(2, std::min(8, std::atoi(e)));
   return r;
 }
@@ -1958,7 +1975,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
                     p->row_count > 1 && p->row_band_log2 < 3 ? p->row_stride : 1);
   if (rc) return rc;
   // Launch schedule (samples per pixel per launch): 8, then kLaunchSpp (32) per launch, also
-  // capped by the colour budget (32 B per sample slot, kColourBytes per launch); the last launch
+  // capped by the record budget (64 B per sample slot, kLaunchBytes per launch); the last launch
   // takes a small remainder with it (1920x1080x512: 8, 15 x 32, 24 = 17 launches).  The first
   // render waits only for an 8-sample warm-up; every later warm-up is ~0.15x the render before it,
   // so it finishes underneath.  Each launch ends with the tail of its longest paths (~1 ms), but
@@ -1973,8 +1990,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // a drain.  Neither floor nor cap exceeds the colour budget or 2^31 slots.
   const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
   const uint64_t slot_spp = (kLaunchSlots + nps - 1) / nps;
+  // bytes of a slot's record: the start record, which the colour overwrites (xor128: the colour)
+  const size_t welem = x128 ? 8 * kColStride : (f32 ? sizeof(StartRecF) : sizeof(StartRec));
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>({spp, kColourBytes / (8ull * kColStride * nps),
+      1, std::min<uint64_t>({spp, kLaunchBytes / (welem * nps),
                              std::max<uint64_t>({kLaunchSpp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
   for (uint32_t s0 = 0, k = std::min(kFirstLaunch, kmax); s0 < spp;) {
@@ -1991,8 +2010,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   }
   uint32_t K = 0;  // largest launch
   for (auto& l : sched) K = std::max(K, l.second);
+  // a buffer follows the call: grown when it is too small, and given back when the call needs
+  // less than half of it (device_bytes then reports about what the call holds)
   auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t elem) -> int {
-    if (need <= cap) return YK_OK;
+    if (need <= cap && 2 * need >= cap) return YK_OK;
     (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
@@ -2001,17 +2022,16 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     return YK_OK;
   };
   const uint32_t nlaunch = (uint32_t)sched.size();
-  // warm-up records: each sample's whole start (StartRec, FP32 StartRecF)
-  const size_t welem = f32 ? sizeof(StartRecF) : sizeof(StartRec);  // per sample slot
-  uint32_t kWarmRing = (uint32_t)std::min<uint64_t>(
-      nlaunch, std::max<uint64_t>(3, kWarmBytes / (welem * nps * K)));
-  if (const char* e = std::getenv("YKGPU_WARM_RING"))  // (A/B) launches of start records ahead
+  // start records (StartRec, FP32 StartRecF: each sample's whole start), the colours written over
+  // them: warm-up c fills buffer c % ring after the reduce of launch c - ring has read it
+  uint32_t kWarmRing = std::min(nlaunch, kWarmRingDepth);
+  if (const char* e = std::getenv("YKGPU_WARM_RING"))  // (A/B) launch buffers in the ring
     kWarmRing = (uint32_t)std::min<uint64_t>(nlaunch, (uint64_t)std::max(2, std::atoi(e)));
+  // xor128: colour buffers only; render c writes buffer c % ring and waits for the reduce of launch
+  // c - ring; reduce c (stream red) overlaps the renders after it
+  const uint32_t kColRing = x128 ? std::min(nlaunch, col_ring()) : kWarmRing;
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
-  // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
-  // reduce c (stream red) overlaps the renders after it
-  const uint32_t kColRing = col_ring(nps, K);
-  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)kColRing * nps * K * kColStride, sizeof(double)))) return rc;
+  if (x128 && (rc = grow(ctx->d_col, ctx->col_cap, (size_t)kColRing * nps * K * kColStride, sizeof(double)))) return rc;
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
@@ -2111,7 +2131,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ra.sums = sums_dev;
   ra.npix_slots = nps;
   ra.spp = spp;
-  ra.pad0 = ra.pad1 = 0;
+  ra.cstride = (uint32_t)(welem / 8);
+  ra.pad1 = 0;
   // one slot counter per launch, all cleared here: a clear between launches is a fill kernel
   // that waits for a free CU behind the warm-ups and reduces (up to 1.6 ms per launch, measured)
   if (nlaunch > ctx->counter_cap) {
@@ -2139,7 +2160,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   YK_HIP(hipStreamWaitEvent(ctx->ren, ctx->ev0, 0));
   auto warm = [&](uint32_t c) -> int {
     hipEvent_t* ev = &ctx->lev[6 * c];
-    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
+    // its buffer: the reduce of launch c - ring has read the colours there
+    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 5], 0));
     wa.s0 = sched[c].first;
     wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
@@ -2166,11 +2188,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     hipEvent_t* ev = &ctx->lev[6 * c];
     const uint32_t s0 = sched[c].first, ks = sched[c].second;
     const uint32_t nsl = nps * ks;
-    double* col = ctx->d_col + (size_t)(c % kColRing) * nps * K * kColStride;
+    // colour records: over the launch's start records (xor128: its colour buffer)
+    char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
+    double* col = x128 ? ctx->d_col + (size_t)(c % kColRing) * nps * K * kColStride : (double*)wring;
     ka.s0 = s0;
     ka.nsl = nsl;
     ka.col = col;
-    char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
     ka.start = (const void*)wring;
     // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
     // only on its own start records and colour buffer, so its blocks take the CUs that launch c's
@@ -2180,7 +2203,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (c & 1) * lanes * ykd::kMtN : nullptr;
     ka.id_scratch = ctx->d_ids + (c & 1) * lanes * ctx->id_stride;
     YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its start records
-    if (c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
+    if (x128 && c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
     ka.pixel_counter = ctx->d_counter + c;
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
@@ -2213,6 +2236,20 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ctx->stats.launches = launches;
   ctx->stats.grid_blocks = (uint32_t)grid;
   ctx->stats.seed_key = seed_key;
+  // what this call needed (device_bytes: what the context holds)
+  {
+    const uint64_t lanes = (uint64_t)grid * block;
+    uint64_t cb = ctx->t64.bytes + ctx->t32.bytes +
+                  (uint64_t)ctx->nspheres * (sizeof(SphereGeo) + sizeof(SphereMat) + sizeof(float4));
+    cb += x128 ? (uint64_t)kColRing * nps * K * kColStride * sizeof(double) : (uint64_t)kWarmRing * nps * K * welem;
+    cb += (nlaunch > 1 ? (uint64_t)nps * 3 * sizeof(double) : 0) + (uint64_t)nps * sizeof(uint32_t);
+    cb += nlaunch * sizeof(uint32_t) + kCounters * sizeof(unsigned long long);
+    if (!x128) cb += 2 * lanes * ykd::kMtN * sizeof(uint32_t);
+    cb += 2 * lanes * std::max(1u, p->max_depth > kStackRegs ? p->max_depth : 1u) * sizeof(uint16_t);
+    const uint64_t npix = (uint64_t)p->row_count * p->image_width;
+    cb += npix * 3 + (sums_dev ? npix * 3 * sizeof(double) : 0);
+    ctx->stats.call_bytes = cb;
+  }
   ctx->stats_pending = true;
   return YK_OK;
 }
@@ -2286,9 +2323,10 @@ int finish_stats(ykgpu_context* ctx) {
 // instances of workgroup size v (kBlock, kBlockX128) that read the tree from global memory / LDS
 // (for the occupancy).
 int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
-                double cam_ext, const ykbvh::Options& opt, const void* geo, size_t elem, size_t tgeo_elem,
-                const RenderKernel (&kern)[2][2]) {
+                double cam_ext, const ykbvh::Options& opt, uint32_t leaf_cap, const void* geo, size_t elem,
+                size_t tgeo_elem, const RenderKernel (&kern)[2][2]) {
   const uint32_t count = (uint32_t)radii.size();
+  if (opt.max_leaf > leaf_cap) return fail(YK_ERR_UNSUPPORTED, "BVH leaf size above the kernel's leaf capacity");
   const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
   if (bvh.depth > ykbvh::kMaxDepth) return fail(YK_ERR_INVALID, "BVH deeper than the traversal stack");
   std::vector<char> leaf_geo(count * elem);
@@ -2298,6 +2336,12 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   int32_t root_code = 0;
   uint32_t wdepth = 0;
   const std::vector<DevNode> snodes = ykbvh::wide_nodes(bvh, &root_code, &wdepth);
+  // every leaf the kernel can reach must fit its leaf code (kLeafCapF64 / kLeafCapF32)
+  auto leaf_fits = [&](int32_t code) { return code >= 0 || (((~(uint32_t)code) & 15u) <= leaf_cap); };
+  bool fits = leaf_fits(root_code);
+  for (const DevNode& w : snodes)
+    for (int k = 0; k < 4; ++k) fits = fits && leaf_fits(w.child[k]);
+  if (!fits) return fail(YK_ERR_UNSUPPORTED, "a BVH leaf holds more spheres than the kernel's leaf code tests");
   const size_t nn = std::max<size_t>(1, snodes.size());
   YK_HIP(hipMalloc(&t.nodes, nn * sizeof(DevNode)));
   YK_HIP(hipMalloc(&t.leaf_geo, count * elem));
@@ -2463,6 +2507,9 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   // its own stream (the diagnostic entry points), not for the rest of the device
   YK_HIP(hipEventSynchronize(ctx->ev1));
   YK_HIP(hipStreamSynchronize(ctx->stream));
+  // ... and for every stream of the context: a launch() that failed part-way may have queued
+  // warm-ups, renders or reduces without recording ev1 (still not the rest of the device)
+  for (hipStream_t s : {ctx->aux, ctx->red, ctx->ren, ctx->alt}) YK_HIP(hipStreamSynchronize(s));
   if (count > ctx->nspheres || !ctx->d_geo) {
     (void)hipFree(ctx->d_geo);
     (void)hipFree(ctx->d_mat);
@@ -2490,24 +2537,25 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   // one sphere per leaf for the 4-wide FP64 tree: 64-spp A/B on the final scene 32.5 -> 31.7 ms
   // against two (three: 33.4); the FP32 tree keeps two (one or three: neutral)
   ykbvh::Options bopt;
-  bopt.max_leaf = 1;  // the FP64 kernel tests one sphere per leaf, without a loop
+  bopt.max_leaf = kLeafCapF64;  // the FP64 kernel tests one sphere per leaf, without a loop
   if (const char* e = std::getenv("YKGPU_BVH_BINS")) bopt.bins = std::max(2, std::min(256, std::atoi(e)));  // (A/B)
   // SAH over all three axes: 512-spp A/B 199.4 -> 198.3 ms (model: 5.51 -> 5.13 visits per segment)
   bopt.all_axes = true;
   if (const char* e = std::getenv("YKGPU_BVH_ALLAXES")) bopt.all_axes = std::atoi(e) != 0;                  // (A/B)
   const RenderKernel k64[2][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
                                   {fp64_kernel(false, 4), fp64_kernel(true, 4)}};
-  int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, geo.data(), sizeof(SphereGeo),
+  int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, kLeafCapF64, geo.data(), sizeof(SphereGeo),
                        sizeof(SphereGeo), k64);
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
-  fopt.max_leaf = 2;  // the FP32 kernel's leaf loop is unrolled for two spheres
+  fopt.max_leaf = kLeafCapF32;  // the FP32 kernel's leaf loop is unrolled for two spheres
   if (const char* e = std::getenv("YKGPU_BVH_ALLAXES_F32")) fopt.all_axes = std::atoi(e) != 0;  // (A/B; on: neutral)
   fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
   fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
   const RenderKernel k32[2][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
                                   {f32_kernel(false, 4), f32_kernel(true, 4)}};
-  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, geo_f.data(), sizeof(float4), sizeof(float4), k32);
+  rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, kLeafCapF32, geo_f.data(), sizeof(float4),
+                   sizeof(float4), k32);
   if (rc) return rc;
   // the float bound assumes neither underflow nor overflow: a scene outside that
   // scale renders FP32 with the linear scan throughout
@@ -2799,6 +2847,7 @@ int ykgpu_group_render(ykgpu_group* g, const yk_render_params* p, uint8_t* rgb_h
     tot.resolve_ms = std::max(tot.resolve_ms, s.resolve_ms);
     tot.seed_key = s.seed_key;
     tot.device_bytes += s.device_bytes + g->tile_cap[e];
+    tot.call_bytes += s.call_bytes + rows[e] * row_bytes;
   }
   tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   g->total = tot;

@@ -113,6 +113,7 @@ class RenderStats(ctypes.Structure):
         ("render_busy_ms", ctypes.c_double),
         ("work", ctypes.c_uint64 * 8),
         ("device_bytes", ctypes.c_uint64),
+        ("call_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -127,7 +128,7 @@ class RenderStats(ctypes.Structure):
 assert ctypes.sizeof(Sphere) == 80
 assert ctypes.sizeof(Camera) == 19 * 8
 assert ctypes.sizeof(RenderParams) == 72
-assert ctypes.sizeof(RenderStats) == 320
+assert ctypes.sizeof(RenderStats) == 328
 
 
 def image_height_for(width: int) -> int:
