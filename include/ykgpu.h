@@ -242,6 +242,10 @@ int ykgpu_math_sqrt_f32(ykgpu_context* ctx, const float* in, float* out, uint64_
  * sphere.hpp / vec3.hpp) on n host triples: out3[3i+k] = num3[3i+k] / den[i].  It must equal
  * IEEE division bit for bit; the tests check it. */
 int ykgpu_math_div(ykgpu_context* ctx, const double* num3, const double* den, double* out3, uint64_t n);
+/* Diagnostic: the FP32 kernel's vector / scalar division (ykf::divs_fast: the compiler's float
+ * division without its special-case steps, the reciprocal shared by the three components) on n
+ * (3 numerators, denominator) pairs: out3 must equal num3 / den in IEEE float, bit for bit. */
+int ykgpu_math_div_f32(ykgpu_context* ctx, const float* num3, const float* den, float* out3, uint64_t n);
 
 /* Statistics of the last render on this context. */
 int ykgpu_get_stats(ykgpu_context* ctx, yk_render_stats* out);

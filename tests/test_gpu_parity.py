@@ -109,6 +109,45 @@ def test_fast_division_is_ieee_division(ren):
     assert bad.size == 0, [(num[i, j], den[i], got[i, j], want[i, j]) for i, j in bad[:5]]
 
 
+@pytest.mark.gpu
+def test_fast_float_division_is_ieee_division(ren):
+    """The FP32 path's vector / scalar division skips div_scale / div_fmas / div_fixup for
+    operands in [2^-40, 2^40] and shares the refined reciprocal (yk_device_f32.hpp); it must be
+    IEEE float division bit for bit: every significand of the divisor in [1, 2) against random
+    numerators, random operands of every sign and exponent, both sides of the range edges, zeros,
+    subnormals and infinities (those take the full-division fallback)."""
+    rng = np.random.default_rng(5)
+    f = np.float32
+
+    def draw(size, lo, hi):
+        v = np.ldexp(1.0 + rng.random(size), rng.integers(lo, hi, size)).astype(f)
+        return np.where(rng.random(size) < 0.5, -v, v).astype(f)
+
+    # every float divisor in [1, 2) (2^23 significands), numerators in the renderer's magnitudes
+    sig = (np.arange(1 << 23, dtype=np.uint32) | np.uint32(0x3F800000)).view(f)
+    num = draw((sig.size, 3), -3, 3)
+    den = sig.copy()
+    extra = 1 << 20
+    num2 = draw((extra, 3), -60, 60)
+    den2 = draw(extra, -60, 60)
+    lo, hi = f(2.0 ** -40), f(2.0 ** 40)
+    edges = np.array([lo, hi, np.nextafter(lo, f(0)), np.nextafter(hi, f(np.inf))], dtype=f)
+    k = np.arange(4096)
+    num2[:4096] = edges[k % 4, None] * np.array([1.0, -1.0, 3.0], dtype=f)
+    den2[:4096] = edges[(k // 4) % 4] * np.where(k % 3 == 0, f(-1.0), f(1.0))
+    special = np.array([0.0, -0.0, 1e-45, -1e-45, np.inf, -np.inf, 1.0, -2.5], dtype=f)
+    num2[8192:8192 + 512] = special[rng.integers(0, 8, (512, 3))]
+    den2[8192:8192 + 512] = special[rng.integers(4, 8, 512)]
+    num = np.concatenate([num, num2]).astype(f)
+    den = np.concatenate([den, den2]).astype(f)
+    got = ren.math_div_f32(num, den)
+    with np.errstate(all="ignore"):
+        want = (num / den[:, None]).astype(f)
+    same = (got.view(np.int32) == want.view(np.int32)) | (np.isnan(got) & np.isnan(want))
+    bad = np.argwhere(~same)
+    assert bad.size == 0, [(num[i, j], den[i], got[i, j], want[i, j]) for i, j in bad[:5]]
+
+
 EXT = [("rtiow5", 0, 80, 45, 16, 50), ("final", 42, 64, 36, 8, 50),
        ("glass", 42, 48, 27, 8, 200), ("final", 7, 40, 22, 12, 10)]
 

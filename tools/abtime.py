@@ -24,7 +24,9 @@ img = r.render(p); ts = []
 for _ in range(int(sys.argv[2])):
     t = time.perf_counter(); r.render(p); ts.append(time.perf_counter() - t)
 import hashlib
-print(json.dumps({"ms": round(min(ts) * 1e3, 3), "kernel_ms": round(r.stats()["kernel_ms"], 3),
+st = r.stats()
+print(json.dumps({"ms": round(min(ts) * 1e3, 3), "kernel_ms": round(st["kernel_ms"], 3),
+                  "render_busy_ms": round(st["render_busy_ms"], 3), "call_gb": round(st["call_bytes"] / 1e9, 2),
                   "sha": hashlib.sha256(img.tobytes()).hexdigest()[:12]}))
 ''' % ROOT
 spp = sys.argv[1]

@@ -26,7 +26,7 @@ CLI_PATH = os.path.join(LIB_DIR, "raytrace")
 EXPORTS = (
     "ykgpu_abi_version", "ykgpu_last_error", "ykgpu_device_count", "ykgpu_context_create",
     "ykgpu_context_destroy", "ykgpu_set_scene", "ykgpu_render", "ykgpu_render_async",
-    "ykgpu_render_sums", "ykgpu_render_trace", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_sqrt_f32", "ykgpu_math_div", "yk_camera_reference", "yk_camera_look",
+    "ykgpu_render_sums", "ykgpu_render_trace", "ykgpu_get_stats", "ykgpu_math_sqrt", "ykgpu_math_sqrt_f32", "ykgpu_math_div", "ykgpu_math_div_f32", "yk_camera_reference", "yk_camera_look",
     "yk_scene_build", "yk_scene_write", "yk_scene_read", "yk_image_height_for",
     "ykgpu_group_create", "ykgpu_group_destroy", "ykgpu_group_size", "ykgpu_group_set_scene",
     "ykgpu_group_render", "ykgpu_group_get_stats", "ykgpu_render_devices",
@@ -74,6 +74,7 @@ def load_library():
         "ykgpu_math_sqrt": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
         "ykgpu_math_sqrt_f32": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
         "ykgpu_math_div": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
+        "ykgpu_math_div_f32": ([c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_uint64], c.c_int),
         "yk_camera_reference": ([P(Camera)], c.c_int),
         "yk_camera_look": ([P(Camera), P(c.c_double), P(c.c_double), P(c.c_double), c.c_double,
                             c.c_double, c.c_double, c.c_double], c.c_int),
@@ -222,6 +223,15 @@ class Renderer:
         assert a.shape[0] == b.shape[0]
         out = np.empty_like(a)
         _check(self._lib.ykgpu_math_div(self._ctx, a.ctypes.data, b.ctypes.data, out.ctypes.data, b.size))
+        return out
+
+    def math_div_f32(self, num3, den) -> np.ndarray:
+        """The FP32 path's vector / scalar division: num3[i, k] / den[i] in float (diagnostic)."""
+        a = np.ascontiguousarray(num3, dtype=np.float32).reshape(-1, 3)
+        b = np.ascontiguousarray(den, dtype=np.float32).reshape(-1)
+        assert a.shape[0] == b.shape[0]
+        out = np.empty_like(a)
+        _check(self._lib.ykgpu_math_div_f32(self._ctx, a.ctypes.data, b.ctypes.data, out.ctypes.data, b.size))
         return out
 
     def stats(self) -> dict:

@@ -31,6 +31,38 @@ __device__ __forceinline__ float len2(v3 a) { return a.x * a.x + a.y * a.y + a.z
 __device__ __forceinline__ v3 of(const double* p) { return {(float)p[0], (float)p[1], (float)p[2]}; }
 __device__ __forceinline__ v3 off(const float* p) { return {p[0], p[1], p[2]}; }
 
+// ---- float division without the special-case steps (the FP64 divs_fast's argument, yk_device.hpp)
+// The compiler's correctly rounded float division on gfx950 is
+//   div_scale(d), div_scale(n), rcp, fma, fma (refined reciprocal), mul, fma, fma, fma (two
+//   residual corrections), div_fmas, div_fixup                        (11 instructions)
+// div_scale rescales only when an exponent is extreme (|n / d| >= 2^96, d or 1/d or n / d
+// denormal, |n| < 2^-104), div_fmas is then a plain fma, and div_fixup only rewrites NaN, inf,
+// zero and denormal cases: for |n|, |d| in [2^-40, 2^40] (or n == 0) the sequence below is the same
+// arithmetic minus those three steps, and the refined reciprocal, which depends only on d, serves
+// every component of a vector.  A zero numerator's sign is fixed as in ykd::div_by.  Checked bit
+// for bit against IEEE float division on the GPU (ykgpu_math_div_f32,
+// tests/test_gpu_parity.py::test_fast_float_division_is_ieee_division).
+__device__ __forceinline__ bool div_range(float x) { return fabsf(x) >= 0x1p-40f && fabsf(x) <= 0x1p40f; }
+__device__ __forceinline__ bool num_range(float x) { return x == 0.0f || div_range(x); }
+__device__ __forceinline__ float rcp_refined(float d) {
+  const float r0 = __builtin_amdgcn_rcpf(d);
+  return __builtin_fmaf(__builtin_fmaf(-d, r0, 1.0f), r0, r0);
+}
+__device__ __forceinline__ float div_by(float n, float d, float r) {
+  const float q0 = n * r;
+  const float q1 = __builtin_fmaf(__builtin_fmaf(-d, q0, n), r, q0);
+  return __builtin_copysignf(__builtin_fmaf(__builtin_fmaf(-d, q1, n), r, q1), q0);
+}
+// vector / scalar with the shared reciprocal r = rcp_refined(d); a wave with any operand out of
+// range recomputes with the full division (same bits for the in-range lanes)
+__device__ __forceinline__ v3 divs_fast_r(v3 a, float d, float r) {
+  v3 q = {div_by(a.x, d, r), div_by(a.y, d, r), div_by(a.z, d, r)};
+  const bool ok = div_range(d) && num_range(a.x) && num_range(a.y) && num_range(a.z);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) q = divs(a, d);
+  return q;
+}
+__device__ __forceinline__ v3 divs_fast(v3 a, float d) { return divs_fast_r(a, d, rcp_refined(d)); }
+
 // math::sqrt<float> (math.hpp:10-19): `T x = s / 2.0` and `x = (x + s / x) / 2.0` halve in
 // double and round to float, which equals the float product by 0.5f (halving is exact, so both
 // are one rounding of the same value).  As for FP64 (yk_device.hpp), the loop's result is a
@@ -45,7 +77,9 @@ __device__ __forceinline__ float nsqrt(float s, uint32_t& iters) {
   if (s >= 0x1p-100f && s <= 0x1p100f) {
     const float r = __builtin_sqrtf(s);
     ++iters;
-    return (r + s / r) * 0.5f;
+    // s / r without div_scale / div_fmas / div_fixup: for s in [2^-100, 2^100], r, 1/r and s / r
+    // lie in [2^-50, 2^50], where none of them changes anything (see div_by)
+    return (r + div_by(s, r, rcp_refined(r))) * 0.5f;
   }
   float x = s * 0.5f;
   float prev = 0.0f;

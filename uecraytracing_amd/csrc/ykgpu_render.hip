@@ -72,7 +72,8 @@ struct alignas(32) SphereGeo {
 struct alignas(16) SphereMat {
   double ar, ag, ab, fuzz;
   double radius, ior;
-  uint32_t kind, pad0;
+  uint32_t kind;
+  float inv_rf;  // ykf::rcp_refined((float)radius) (FP32 kernel), computed on the device by yk_mat_prep
   double inv_r;  // ykd::rcp_refined(radius), computed on the device by yk_mat_prep
 };
 static_assert(sizeof(SphereMat) == 64, "SphereMat layout");
@@ -105,6 +106,10 @@ constexpr int mode_block() {
 constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #ifndef YK_RENDER_PRIO
 #define YK_RENDER_PRIO 1
+#endif
+// the FP64 visit's slab constants as one op_sel-read register pair per axis and bound (yk_slab.hpp)
+#ifndef YK_SLAB_PAIRS
+#define YK_SLAB_PAIRS 1
 #endif
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
@@ -232,6 +237,8 @@ __device__ __noinline__ Hit scan_linear(const SphereGeo* __restrict__ geo, uint3
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+
+#include "yk_slab.hpp"
 
 __device__ __forceinline__ float safe_rcp(float x) {
   return fabsf(x) > 1e-30f ? 1.0f / x : copysignf(1e30f, x);
@@ -434,16 +441,14 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 // into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
 
-// A sample's colour record: r, g, b (one 16-byte and one 8-byte store) at the start of a
-// kStride-double record per sample slot.  The mt19937 kernels write it over the slot's own
-// StartRec (64 B; FP32: StartRecF, 48 B): the lane read the whole record when the path started,
-// so a launch needs no colour buffer of its own; xor128 launches, which have no
-// start records, write 32-byte records into a colour ring.  yk_reduce_samples reads the records
-// of consecutive slots.
-constexpr size_t kColStride = 4;  // xor128's colour records (doubles)
-template <size_t kStride>
+// A sample's colour record: r, g, b as one aligned 32-byte record per sample slot (one 16-byte
+// and one 8-byte store, the whole record in one 32-byte sector), in a colour buffer of the launch.
+// yk_reduce_samples reads the records of consecutive slots, coalesced.  (Round 4 tried writing
+// the colour over the slot's own StartRec instead — no colour buffer at all — and the frame got
+// 3% slower: 174.1 -> 179.5 ms, profiles/r04_ab/; the reduce then reads 24 of every 64 bytes.)
+constexpr size_t kColStride = 4;
 __device__ __forceinline__ void colour_store(double* col, uint32_t slot, double r, double g, double b) {
-  double* rec = col + (size_t)slot * kStride;
+  double* rec = col + (size_t)slot * kColStride;
   *(double2*)rec = make_double2(r, g);
   rec[2] = b;
 }
@@ -453,13 +458,13 @@ __device__ __forceinline__ void colour_store(double* col, uint32_t slot, double 
 // the last launch, to_color3b (source.cpp:73-83): /spp, math::sqrt, clamp [0, .999], *256,
 // truncate.  One thread per processing slot, coalesced over the SoA colours.
 struct ReduceArgs {
-  const double* col;  // col[(s_local * npix_slots + p) * cstride + c]
+  const double* col;  // col[(s_local * npix_slots + p) * kColStride + c]
   double* acc;        // running sums, acc[c * npix_slots + p]
   const uint32_t* order;
   uint8_t* rgb;
   double* sums;
   uint32_t npix_slots, nsl, ks, spp;
-  uint32_t first, last, cstride, pad1;  // cstride: doubles per colour record
+  uint32_t first, last, pad0, pad1;
 };
 __device__ __forceinline__ void reduce_slot(const ReduceArgs& ra, uint32_t p) {
   const uint32_t q = ra.order[p];
@@ -470,7 +475,7 @@ __device__ __forceinline__ void reduce_slot(const ReduceArgs& ra, uint32_t p) {
   for (uint32_t k = 0; k < ra.ks; ++k) {
     const size_t i = (size_t)k * ra.npix_slots + p;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[i * ra.cstride + c];
+    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[i * kColStride + c];
   }
   if (!ra.last) {
 #pragma unroll
@@ -497,7 +502,10 @@ __global__ __launch_bounds__(256) void yk_reduce_samples(ReduceArgs ra) {
 // divs_fast).  Run once per set_scene.
 __global__ void yk_mat_prep(SphereMat* m, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) m[i].inv_r = ykd::rcp_refined(m[i].radius);
+  if (i < n) {
+    m[i].inv_r = ykd::rcp_refined(m[i].radius);
+    m[i].inv_rf = ykf::rcp_refined((float)m[i].radius);
+  }
 }
 
 // ykgpu_math_div: the renderer's vector / scalar division (divs_fast) on a buffer (diagnostic).
@@ -506,6 +514,16 @@ __global__ __launch_bounds__(256) void yk_math_div(const double* num3, const dou
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const ykd::v3 q = ykd::divs_fast({num3[3 * i], num3[3 * i + 1], num3[3 * i + 2]}, den[i]);
+  out3[3 * i] = q.x;
+  out3[3 * i + 1] = q.y;
+  out3[3 * i + 2] = q.z;
+}
+
+// ykgpu_math_div_f32: the FP32 kernel's vector / scalar division (ykf::divs_fast) on a buffer.
+__global__ __launch_bounds__(256) void yk_math_div_f32(const float* num3, const float* den, float* out3, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ykf::v3 q = ykf::divs_fast({num3[3 * i], num3[3 * i + 1], num3[3 * i + 2]}, den[i]);
   out3[3 * i] = q.x;
   out3[3 * i + 1] = q.y;
   out3[3 * i + 2] = q.z;
@@ -573,6 +591,9 @@ __attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
 // production instances at <= 128 VGPRs (one short of their natural 129): 3 x 128 of a SIMD's 512
 // leave 128, four yk_mt_warmup waves of 32 (the counting instances keep their registers)
 __attribute__((amdgpu_waves_per_eu((kMode & 1) ? 1 : 4, 8)))
+#endif
+#ifdef YK_SINGLE_VGPRS
+__attribute__((amdgpu_num_vgpr(YK_SINGLE_VGPRS / 2)))  // (A/B; gfx950 counts the unified file: x2)
 #endif
 void yk_render_persistent(KernelArgs ka) {
   constexpr int kBlk = mode_block<kMode>();
@@ -762,16 +783,23 @@ void yk_render_persistent(KernelArgs ka) {
         //   max(tn, tmin_lo) <= min(tf * c, ustar_f),
         // which holds whenever the former test with both distances relaxed by 2^-20 held.
         constexpr float kFar = 1.0f + 0x1p-17f;
-        const f2 ixv = {ix, ix}, iyv = {iy, iy}, izv = {iz, iz};
-        const f2 noix = {-oix, -oix}, noiy = {-oiy, -oiy}, noiz = {-oiz, -oiz};
         // scaled far terms: ONE rounding of the origin product, as for the near terms, so the
         // origin perturbation stays within delta/4 (yk_bvh.hpp); the rounding of ix*c is a
         // relative error inside the 2^-17 margin
         const float ixs = ix * kFar, iys = iy * kFar, izs = iz * kFar;
-        const f2 ixc = {ixs, ixs}, iyc = {iys, iys}, izc = {izs, izs};
         const float ox_f = (float)o.x, oy_f = (float)o.y, oz_f = (float)o.z;
+#if YK_SLAB_PAIRS
+        // per axis ONE register pair (1/d, -o/d) (near) and (c/d, -o c/d) (far), read by op_sel
+        // (yk_slab.hpp): 12 VGPRs instead of 24
+        const f2 sxp = {ix, -oix}, syp = {iy, -oiy}, szp = {iz, -oiz};
+        const f2 fxp = {ixs, -(ox_f * ixs)}, fyp = {iys, -(oy_f * iys)}, fzp = {izs, -(oz_f * izs)};
+#else
+        const f2 ixv = {ix, ix}, iyv = {iy, iy}, izv = {iz, iz};
+        const f2 noix = {-oix, -oix}, noiy = {-oiy, -oiy}, noiz = {-oiz, -oiz};
+        const f2 ixc = {ixs, ixs}, iyc = {iys, iys}, izc = {izs, izs};
         const f2 noixc = {-(ox_f * ixs), -(ox_f * ixs)}, noiyc = {-(oy_f * iys), -(oy_f * iys)},
                  noizc = {-(oz_f * izs), -(oz_f * izs)};
+#endif
         const double ia = ykd::rcp_bound(a);  // bounds only: relative error < 2^-44
         const float tmin_lo = __double2float_rd(ka.t_min) * (1.0f - 0x1p-17f);
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
@@ -798,19 +826,34 @@ void yk_render_persistent(KernelArgs ka) {
             const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
             const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
             const int4 ch = *(const int4*)(nodes + node + 144);
+            bool hk[4];
+#if YK_SLAB_PAIRS
+            const f2 nx[2] = {slab_fma(qnx.xy, sxp), slab_fma(qnx.zw, sxp)};
+            const f2 fx[2] = {slab_fma(qfx.xy, fxp), slab_fma(qfx.zw, fxp)};
+            const f2 ny[2] = {slab_fma(qny.xy, syp), slab_fma(qny.zw, syp)};
+            const f2 fy[2] = {slab_fma(qfy.xy, fyp), slab_fma(qfy.zw, fyp)};
+            const f2 nz[2] = {slab_fma(qnz.xy, szp), slab_fma(qnz.zw, szp)};
+            const f2 fz[2] = {slab_fma(qfz.xy, fzp), slab_fma(qfz.zw, fzp)};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float tn = slab_max(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]), tmin_lo);
+              const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
+              hk[k] = tn <= tf;
+            }
+#else
             const f2 nx[2] = {__builtin_elementwise_fma(qnx.xy, ixv, noix), __builtin_elementwise_fma(qnx.zw, ixv, noix)};
             const f2 fx[2] = {__builtin_elementwise_fma(qfx.xy, ixc, noixc), __builtin_elementwise_fma(qfx.zw, ixc, noixc)};
             const f2 ny[2] = {__builtin_elementwise_fma(qny.xy, iyv, noiy), __builtin_elementwise_fma(qny.zw, iyv, noiy)};
             const f2 fy[2] = {__builtin_elementwise_fma(qfy.xy, iyc, noiyc), __builtin_elementwise_fma(qfy.zw, iyc, noiyc)};
             const f2 nz[2] = {__builtin_elementwise_fma(qnz.xy, izv, noiz), __builtin_elementwise_fma(qnz.zw, izv, noiz)};
             const f2 fz[2] = {__builtin_elementwise_fma(qfz.xy, izc, noizc), __builtin_elementwise_fma(qfz.zw, izc, noizc)};
-            bool hk[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const float tn = fmaxf(fmaxf(fmaxf(nx[k >> 1][k & 1], ny[k >> 1][k & 1]), nz[k >> 1][k & 1]), tmin_lo);
               const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
+#endif
             // keep the child-code read in this block, issued with the plane reads (the compiler
             // would otherwise sink it into the branch below and wait for it there)
             asm volatile("" ::"v"(ch.x), "v"(ch.y), "v"(ch.z), "v"(ch.w));
@@ -1081,10 +1124,8 @@ void yk_render_persistent(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
-      // the sample's colour (over its StartRec for mt19937); yk_reduce_samples adds them in
-      // sample order
-      colour_store<std::is_same<Gen, ykd::MtLane>::value ? sizeof(StartRec) / 8 : kColStride>(ka.col, slot, L_r,
-                                                                                             L_g, L_b);
+      // the sample's colour; yk_reduce_samples adds them in sample order
+      colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
     YK_STAMP(5);
@@ -1121,6 +1162,8 @@ RenderKernel fp64_kernel(bool lds, int mode) {
   return k[(lds ? 8 : 0) + (mode & 7)];
 }
 
+#include "yk_dual.hpp"
+
 // ---- render<float> (YK_PRECISION_FP32) ---------------------------------------------------
 // The same persistent, sample-parallel structure as yk_render_persistent (refill, slots, start
 // records from yk_mt_warmup, attenuation-id stack, SoA colours reduced by yk_reduce_samples),
@@ -1136,17 +1179,24 @@ __device__ __forceinline__ float f_uniform01(G& g) { return ykf::uniform(g, 0.0f
 // sphere::hit_impl<float> (sphere.hpp:25-48) bit for bit, without t_max.  Returns 2 with the root
 // in r (root1 if >= tmin, else root2: the reference accepts it iff r <= t_max, because root2 >=
 // root1 under monotonic rounding), 1 when both roots lie below tmin, 0 when disc < 0.
-__device__ __forceinline__ int f32_root(float4 sg, ykf::v3 o, ykf::v3 d, float a, float tmin, float& r,
-                                        uint32_t& nit) {
+// n / a for a root, a's refined reciprocal ra shared by the ray's candidates (ykf::div_by); a wave
+// with any lane out of range takes the full division
+__device__ __forceinline__ float f32_root_div(float n, float a, float ra, bool a_ok) {
+  float q = ykf::div_by(n, a, ra);
+  if (__builtin_expect(__ballot(!(a_ok && ykf::num_range(n))) != 0, 0)) q = n / a;
+  return q;
+}
+__device__ __forceinline__ int f32_root(float4 sg, ykf::v3 o, ykf::v3 d, float a, float ra, bool a_ok, float tmin,
+                                        float& r, uint32_t& nit) {
   const ykf::v3 oc = {o.x - sg.x, o.y - sg.y, o.z - sg.z};
   const float hb = ykf::dot(oc, d);
   const float c = ykf::len2(oc) - sg.w;
   const float disc = hb * hb - a * c;
   if (disc < 0) return 0;
   const float sq = ykf::nsqrt(disc, nit);
-  r = (-hb - sq) / a;
+  r = f32_root_div(-hb - sq, a, ra, a_ok);
   if (r < tmin) {
-    r = (-hb + sq) / a;
+    r = f32_root_div(-hb + sq, a, ra, a_ok);
     if (r < tmin) return 1;
   }
   return 2;
@@ -1186,10 +1236,17 @@ __device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, 
   const bool far = fabsf(dk) >= kF32FarAt * s;
   const float jf = far ? __builtin_amdgcn_rcpf(dk - sg) * (1.0f + 0x1p-17f) : 0.0f;
   const float nc = -(ok * in), fc = far ? -(ok * jf) : INFINITY;
+#if YK_SLAB_PAIRS
+  // the pairs (in, nc) and (jf, fc), read by op_sel (yk_slab.hpp); nc2 / fc2 unused
+  in2 = f2{in, nc};
+  jf2 = f2{jf, fc};
+  nc2 = fc2 = f2{0.0f, 0.0f};
+#else
   in2 = f2{in, in};
   nc2 = f2{nc, nc};
   jf2 = f2{jf, jf};
   fc2 = f2{fc, fc};
+#endif
 }
 
 // kSceneInLds: the FP32 tree, its float4 leaf geometry and its leaf ids copied into LDS per
@@ -1343,7 +1400,11 @@ void yk_render_f32(KernelArgs ka) {
         // bound like a near distance (same FMA form and error).  Without it, a
         // ray grazing a field of boxes enters every box under its path.  One slow axis per ray
         // gets the bound (y, then x, then z); the others keep L = -inf.
+#if YK_SLAB_PAIRS
+        f2 jl2 = {0.0f, -INFINITY};  // the (jl, cl) pair
+#else
         f2 jl2 = {0.0f, 0.0f}, cl2 = {-INFINITY, -INFINITY};
+#endif
         const char* pl = px + 16;
         {
           const float slow = s * kF32SlowAt;
@@ -1353,8 +1414,12 @@ void yk_render_f32(KernelArgs ka) {
           for (int k = 0; k < 3; ++k) {
             if (fabsf(dk[k]) < slow) {
               const float jl = __builtin_amdgcn_rcpf(dk[k] - (dk[k] < 0.0f ? -s : s));
+#if YK_SLAB_PAIRS
+              jl2 = f2{jl, -(ok[k] * jl)};  // (jl, cl), read by op_sel
+#else
               jl2 = f2{jl, jl};
               cl2 = f2{-(ok[k] * jl), -(ok[k] * jl)};
+#endif
               pl = pk[k] + 16;
             }
           }
@@ -1380,15 +1445,31 @@ void yk_render_f32(KernelArgs ka) {
             const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
             const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
             const int4 ch = *(const int4*)(nodes + node + 144);
+            const f4 qsl = *(const f4*)(pl + node);
+            bool hk[4];
+#if YK_SLAB_PAIRS
+            const f2 nx[2] = {slab_fma(qnx.xy, inx), slab_fma(qnx.zw, inx)};
+            const f2 fx[2] = {slab_fma(qfx.xy, jfx), slab_fma(qfx.zw, jfx)};
+            const f2 ny[2] = {slab_fma(qny.xy, iny), slab_fma(qny.zw, iny)};
+            const f2 fy[2] = {slab_fma(qfy.xy, jfy), slab_fma(qfy.zw, jfy)};
+            const f2 nz[2] = {slab_fma(qnz.xy, inz), slab_fma(qnz.zw, inz)};
+            const f2 fz[2] = {slab_fma(qfz.xy, jfz), slab_fma(qfz.zw, jfz)};
+            const f2 sl[2] = {slab_fma(qsl.xy, jl2), slab_fma(qsl.zw, jl2)};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float tn = slab_max3(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]),
+                                         sl[k >> 1][k & 1], tmin_lo);
+              const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
+              hk[k] = tn <= tf;
+            }
+#else
             const f2 nx[2] = {__builtin_elementwise_fma(qnx.xy, inx, ncx), __builtin_elementwise_fma(qnx.zw, inx, ncx)};
             const f2 fx[2] = {__builtin_elementwise_fma(qfx.xy, jfx, fcx), __builtin_elementwise_fma(qfx.zw, jfx, fcx)};
             const f2 ny[2] = {__builtin_elementwise_fma(qny.xy, iny, ncy), __builtin_elementwise_fma(qny.zw, iny, ncy)};
             const f2 fy[2] = {__builtin_elementwise_fma(qfy.xy, jfy, fcy), __builtin_elementwise_fma(qfy.zw, jfy, fcy)};
             const f2 nz[2] = {__builtin_elementwise_fma(qnz.xy, inz, ncz), __builtin_elementwise_fma(qnz.zw, inz, ncz)};
             const f2 fz[2] = {__builtin_elementwise_fma(qfz.xy, jfz, fcz), __builtin_elementwise_fma(qfz.zw, jfz, fcz)};
-            const f4 qsl = *(const f4*)(pl + node);
             const f2 sl[2] = {__builtin_elementwise_fma(qsl.xy, jl2, cl2), __builtin_elementwise_fma(qsl.zw, jl2, cl2)};
-            bool hk[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               // (a chain: two v_max3)
@@ -1397,6 +1478,7 @@ void yk_render_f32(KernelArgs ka) {
               const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
+#endif
             asm volatile("" ::"v"(ch.x), "v"(ch.y), "v"(ch.z), "v"(ch.w));
             if (hk[0] || hk[1] || hk[2] || hk[3]) {
               node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : ch.x));
@@ -1482,10 +1564,12 @@ void yk_render_f32(KernelArgs ka) {
 #define YK_F32_EVAL(C, L)                                                       \
   if ((L) <= ustar) {                                                           \
     float r = 0.0f;                                                             \
-    const int res = f32_root(geo_f[C], o, d, a, tmin, r, n_nit);                \
+    const int res = f32_root(geo_f[C], o, d, a, ra, a_ok, tmin, r, n_nit);      \
     if (kCount && res > 0) ++n_sqrt, ++n_ncall;                                 \
     if (res == 2 && (r < T || (r == T && (int)(C) > hid))) T = r, hid = (int)(C); \
   }
+          const bool a_ok = ykf::div_range(a);
+          const float ra = ykf::rcp_refined(a);
           if (nc > 0) YK_F32_EVAL(c0, l0)
           if (nc > 1) YK_F32_EVAL(c1, l1)
           if (nc > 2) YK_F32_EVAL(c2, l2)
@@ -1535,7 +1619,7 @@ void yk_render_f32(KernelArgs ka) {
         const float4 sg = geo_f[hid];
         m = mat[hid];
         p = ykf::add(o, ykf::mul(d, T));  // ray::at
-        const ykf::v3 outward = ykf::divs(ykf::sub(p, ykf::v3{sg.x, sg.y, sg.z}), (float)m.radius);
+        const ykf::v3 outward = ykf::divs_fast_r(ykf::sub(p, ykf::v3{sg.x, sg.y, sg.z}), (float)m.radius, m.inv_rf);
         front = ykf::dot(d, outward) < 0;
         nrm = front ? outward : ykf::neg(outward);
       }
@@ -1564,7 +1648,7 @@ void yk_render_f32(KernelArgs ka) {
                                         ykf::uniform_of(c3, -1.0f, 1.0f)};
       const ykf::v3 vn = lamb ? rv : d;
       if (kCount) ++n_ncall;
-      const ykf::v3 un = ykf::divs(vn, ykf::nsqrt(ykf::len2(vn), n_nit));
+      const ykf::v3 un = ykf::divs_fast(vn, ykf::nsqrt(ykf::len2(vn), n_nit));
       float ct = 0;  // dielectric: cos(theta) = min(dot(-unit, n), 1)
       if (diel) {
         ct = ykf::dot(ykf::neg(un), nrm);
@@ -1589,7 +1673,7 @@ void yk_render_f32(KernelArgs ka) {
           nd = ykf::reflect(un, nrm);
           if (fuzzy) {
             const float k = ykf::uniform_of(c0, 0.01f, 0.99f);
-            const ykf::v3 ru = ykf::divs(rv, sq2);
+            const ykf::v3 ru = ykf::divs_fast(rv, sq2);
             nd = ykf::add(nd, ykf::mul(ykf::mul(ru, k), (float)m.fuzz));
           }
           scattered = ykf::dot(nd, nrm) > 0;
@@ -1646,7 +1730,7 @@ void yk_render_f32(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
-      colour_store<kRec ? sizeof(StartRecF) / 8 : kColStride>(ka.col, slot, L_r, L_g, L_b);
+      colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
     YK_STAMP(5);
@@ -1696,13 +1780,14 @@ struct DevTree {
   double origin_bound = 0;  // |o|_inf beyond which a ray takes the linear scan (< 0: every ray)
   uint32_t geo_off = 0, ids_off = 0;  // leaf geometry and ids in LDS, after the nodes
   size_t bytes = 0;                   // device bytes of nodes, leaf geometry and ids
-  // LDS plan per workgroup size: [0] kBlock (mt19937 instances), [1] kBlockX128 (xor128)
+  // LDS plan per kernel shape: [0] kBlock threads (mt19937 instances), [1] kBlockX128 (xor128),
+  // [2] kDualBlock threads with two paths each (yk_render_dual)
   struct Plan {
     bool in_lds = false;
     uint32_t lds_bytes = 0, stack_off = 0, stack_cap = 0, stack_entries = 0;
     uint32_t tgeo_off = 0, mat_off = 0;  // shading tables in LDS (FP64 kernel), 0: none
     int grid = 0;                        // persistent blocks: occupancy x CUs
-  } plan[2];
+  } plan[3];
   void release() {
     (void)hipFree(nodes);
     (void)hipFree(leaf_geo);
@@ -1833,11 +1918,11 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, size_t lanes, bool ne
 #ifndef YK_LAUNCH_MB
 #define YK_LAUNCH_MB 8192
 #endif
-// per-slot records of one launch (start records, which the colours overwrite; xor128: colours)
-// at most: bounds a launch's slots for very large tiles (kmax in launch())
+// colour records of one launch at most: bounds a launch's slots for very large tiles (kmax in
+// launch())
 constexpr uint64_t kLaunchBytes = (uint64_t)YK_LAUNCH_MB << 20;
 // the render kernel addresses a slot's start record as 4 * slot uint4s (FP32: 3) in 32-bit
-// arithmetic: the smallest record (xor128's 32-byte colours) bounds the slot count
+// arithmetic
 static_assert(kLaunchBytes / (8 * kColStride) * 4 < (1ull << 32), "4 * slot must fit 32 bits");
 // samples per pixel per launch at most: many mid-sized launches beat a few big ones, because the
 // launches alternate between two streams and each one's drain overlaps the next one's start
@@ -1857,10 +1942,9 @@ constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
 // Start-record ring: the warm-ups run on ctx->aux, beside the render launches (their wave slots
 // and VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots idle),
-// into a ring of min(launches, kWarmRingDepth) launch buffers (YKGPU_WARM_RING overrides).  The
-// render writes each sample's colour over its start record and the reduce reads it there, so
-// warm-up c waits for the REDUCE of launch c - ring.  Sized to the call: ring x slots x record
-// (1920x1080 at 32 spp per launch: 66M slots x 64 B = 4.2 GB per launch buffer).
+// into a ring of min(launches, kWarmRingDepth) launch buffers (YKGPU_WARM_RING overrides); warm-up
+// c waits for the render of launch c - ring.  Sized to the call: ring x slots x record (1920x1080
+// at 32 spp per launch: 66M slots x 64 B = 4.2 GB per launch buffer).
 #ifndef YK_WARM_RING
 #define YK_WARM_RING 3
 #endif
@@ -1923,10 +2007,13 @@ hipError_t create_render_stream(hipStream_t* s) {
   return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
-// xor128 colour buffers in flight (YKGPU_COL_RING overrides): 3 (the mt19937 kernels write their
-// colours into the start-record ring instead)
+// Colour buffers in flight (YKGPU_COL_RING overrides): render c writes buffer c % ring and waits
+// for the reduce of launch c - ring
+#ifndef YK_COL_RING
+#define YK_COL_RING 4
+#endif
 uint32_t col_ring() {
-  uint32_t r = 3;
+  uint32_t r = YK_COL_RING;
   if (const char* e = std::getenv("YKGPU_COL_RING")) r = (uint32_t)std::max(2, std::min(8, std::atoi(e)));
   return r;
 }
@@ -1951,14 +2038,28 @@ uint32_t warm_per_cu(bool f32) {
   return per_cu;
 }
 
+// yk_render_dual (two paths per lane) for the FP64 mt19937 renders when YKGPU_DUAL=1 (A/B; the
+// production path is the one-path yk_render_persistent: DESIGN.md §8, round 4)
+#ifndef YK_DUAL
+#define YK_DUAL 0
+#endif
+bool dual_enabled() {
+  const char* e = std::getenv("YKGPU_DUAL");
+  return e ? std::atoi(e) != 0 : YK_DUAL != 0;
+}
+
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
   const bool f32 = p->precision == YK_PRECISION_FP32;
   const bool x128 = p->rng == YK_RNG_XOR128;  // no warm-ups, no MT scratch
   const DevTree& tree = f32 ? ctx->t32 : ctx->t64;
-  const DevTree::Plan& plan = tree.plan[x128 ? 1 : 0];
-  const int grid = plan.grid, block = block_of(x128);
-  int rc = ensure_scratch(ctx, p->max_depth, (size_t)grid * block, !x128);
+  // FP64 mt19937: two paths per lane (yk_render_dual) unless YKGPU_DUAL=0 or the one-lane
+  // diagnostic (the single-path counting instance's)
+  const bool dual = !f32 && !x128 && !(p->flags & YK_FLAG_ONE_LANE) && dual_enabled();
+  const DevTree::Plan& plan = tree.plan[dual ? 2 : (x128 ? 1 : 0)];
+  const int grid = plan.grid, block = dual ? kDualBlock : block_of(x128);
+  const int paths = dual ? 2 : 1;  // paths per lane: MT and attenuation scratch per path
+  int rc = ensure_scratch(ctx, p->max_depth, (size_t)grid * block * paths, !x128);
   if (rc) return rc;
   // YK_SEED_RANDOM_DEVICE without a key: one from std::random_device per call (source.cpp:159)
   uint64_t seed_key = 0;
@@ -1975,7 +2076,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
                     p->row_count > 1 && p->row_band_log2 < 3 ? p->row_stride : 1);
   if (rc) return rc;
   // Launch schedule (samples per pixel per launch): 8, then kLaunchSpp (32) per launch, also
-  // capped by the record budget (64 B per sample slot, kLaunchBytes per launch); the last launch
+  // capped by the colour budget (32 B per sample slot, kLaunchBytes per launch); the last launch
   // takes a small remainder with it (1920x1080x512: 8, 15 x 32, 24 = 17 launches).  The first
   // render waits only for an 8-sample warm-up; every later warm-up is ~0.15x the render before it,
   // so it finishes underneath.  Each launch ends with the tail of its longest paths (~1 ms), but
@@ -1990,10 +2091,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // a drain.  Neither floor nor cap exceeds the colour budget or 2^31 slots.
   const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
   const uint64_t slot_spp = (kLaunchSlots + nps - 1) / nps;
-  // bytes of a slot's record: the start record, which the colour overwrites (xor128: the colour)
-  const size_t welem = x128 ? 8 * kColStride : (f32 ? sizeof(StartRecF) : sizeof(StartRec));
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>({spp, kLaunchBytes / (welem * nps),
+      1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
                              std::max<uint64_t>({kLaunchSpp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
   for (uint32_t s0 = 0, k = std::min(kFirstLaunch, kmax); s0 < spp;) {
@@ -2022,16 +2121,21 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     return YK_OK;
   };
   const uint32_t nlaunch = (uint32_t)sched.size();
-  // start records (StartRec, FP32 StartRecF: each sample's whole start), the colours written over
-  // them: warm-up c fills buffer c % ring after the reduce of launch c - ring has read it
+  // start records (StartRec, FP32 StartRecF: each sample's whole start)
+  const size_t welem = f32 ? sizeof(StartRecF) : sizeof(StartRec);
   uint32_t kWarmRing = std::min(nlaunch, kWarmRingDepth);
   if (const char* e = std::getenv("YKGPU_WARM_RING"))  // (A/B) launch buffers in the ring
     kWarmRing = (uint32_t)std::min<uint64_t>(nlaunch, (uint64_t)std::max(2, std::atoi(e)));
-  // xor128: colour buffers only; render c writes buffer c % ring and waits for the reduce of launch
-  // c - ring; reduce c (stream red) overlaps the renders after it
-  const uint32_t kColRing = x128 ? std::min(nlaunch, col_ring()) : kWarmRing;
+  // (diagnostic, timing only) YKGPU_ABL_WARM_FIRST=1: every launch's warm-up runs, and finishes,
+  // before the first render: render_busy_ms then times the render kernels without the seed walks
+  // beside them (same images)
+  const bool warm_first = std::getenv("YKGPU_ABL_WARM_FIRST") != nullptr && !x128;
+  if (warm_first) kWarmRing = nlaunch;
+  // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
+  // reduce c (stream red) overlaps the renders after it
+  const uint32_t kColRing = std::min(nlaunch, col_ring());
   if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
-  if (x128 && (rc = grow(ctx->d_col, ctx->col_cap, (size_t)kColRing * nps * K * kColStride, sizeof(double)))) return rc;
+  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)kColRing * nps * K * kColStride, sizeof(double)))) return rc;
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
@@ -2131,8 +2235,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ra.sums = sums_dev;
   ra.npix_slots = nps;
   ra.spp = spp;
-  ra.cstride = (uint32_t)(welem / 8);
-  ra.pad1 = 0;
+  ra.pad0 = ra.pad1 = 0;
   // one slot counter per launch, all cleared here: a clear between launches is a fill kernel
   // that waits for a free CU behind the warm-ups and reduces (up to 1.6 ms per launch, measured)
   if (nlaunch > ctx->counter_cap) {
@@ -2160,8 +2263,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   YK_HIP(hipStreamWaitEvent(ctx->ren, ctx->ev0, 0));
   auto warm = [&](uint32_t c) -> int {
     hipEvent_t* ev = &ctx->lev[6 * c];
-    // its buffer: the reduce of launch c - ring has read the colours there
-    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 5], 0));
+    // its buffer: the render of launch c - ring has read its records
+    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
     wa.s0 = sched[c].first;
     wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
@@ -2183,14 +2286,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   };
   for (uint32_t c = 0; c < std::min(kWarmRing, nlaunch); ++c)
     if ((rc = warm(c))) return rc;
+  if (warm_first) YK_HIP(hipStreamSynchronize(ctx->aux));
   uint32_t launches = 0;
   for (uint32_t c = 0; c < nlaunch; ++c) {
     hipEvent_t* ev = &ctx->lev[6 * c];
     const uint32_t s0 = sched[c].first, ks = sched[c].second;
     const uint32_t nsl = nps * ks;
-    // colour records: over the launch's start records (xor128: its colour buffer)
     char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
-    double* col = x128 ? ctx->d_col + (size_t)(c % kColRing) * nps * K * kColStride : (double*)wring;
+    double* col = ctx->d_col + (size_t)(c % kColRing) * nps * K * kColStride;
     ka.s0 = s0;
     ka.nsl = nsl;
     ka.col = col;
@@ -2199,17 +2302,20 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     // only on its own start records and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
     const hipStream_t rs = (c & 1) ? ctx->alt : ctx->ren;
-    const size_t lanes = (size_t)grid * block;
+    const size_t lanes = (size_t)grid * block * paths;
     ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (c & 1) * lanes * ykd::kMtN : nullptr;
     ka.id_scratch = ctx->d_ids + (c & 1) * lanes * ctx->id_stride;
     YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its start records
-    if (x128 && c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
+    if (c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
     ka.pixel_counter = ctx->d_counter + c;
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (f32)
       hipLaunchKernelGGL(f32_kernel(plan.in_lds, (count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(block),
                          plan.lds_bytes, rs, ka);
+    else if (dual)
+      hipLaunchKernelGGL(dual_kernel(plan.in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0)),
+                         dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
     else
       hipLaunchKernelGGL(fp64_kernel(plan.in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
                                                       (x128 ? 4 : 0)),
@@ -2238,10 +2344,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ctx->stats.seed_key = seed_key;
   // what this call needed (device_bytes: what the context holds)
   {
-    const uint64_t lanes = (uint64_t)grid * block;
+    const uint64_t lanes = (uint64_t)grid * block * paths;
     uint64_t cb = ctx->t64.bytes + ctx->t32.bytes +
                   (uint64_t)ctx->nspheres * (sizeof(SphereGeo) + sizeof(SphereMat) + sizeof(float4));
-    cb += x128 ? (uint64_t)kColRing * nps * K * kColStride * sizeof(double) : (uint64_t)kWarmRing * nps * K * welem;
+    cb += (uint64_t)kColRing * nps * K * kColStride * sizeof(double) + (x128 ? 0 : (uint64_t)kWarmRing * nps * K * welem);
     cb += (nlaunch > 1 ? (uint64_t)nps * 3 * sizeof(double) : 0) + (uint64_t)nps * sizeof(uint32_t);
     cb += nlaunch * sizeof(uint32_t) + kCounters * sizeof(unsigned long long);
     if (!x128) cb += 2 * lanes * ykd::kMtN * sizeof(uint32_t);
@@ -2324,7 +2430,7 @@ int finish_stats(ykgpu_context* ctx) {
 // (for the occupancy).
 int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
                 double cam_ext, const ykbvh::Options& opt, uint32_t leaf_cap, const void* geo, size_t elem,
-                size_t tgeo_elem, const RenderKernel (&kern)[2][2]) {
+                size_t tgeo_elem, const RenderKernel (&kern)[3][2]) {
   const uint32_t count = (uint32_t)radii.size();
   if (opt.max_leaf > leaf_cap) return fail(YK_ERR_UNSUPPORTED, "BVH leaf size above the kernel's leaf capacity");
   const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
@@ -2366,14 +2472,17 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   const size_t mat_bytes = tgeo_elem ? a16(count * sizeof(SphereMat)) : 0;
   t.geo_off = (uint32_t)a16(t.n_nodes * sizeof(DevNode));
   t.ids_off = t.geo_off + (uint32_t)a16(count * elem);
-  for (int v = 0; v < 2; ++v) {
+  for (int v = 0; v < 3; ++v) {
     DevTree::Plan& pl = t.plan[v];
-    const int blk = block_of(v == 1);
-    // a CU holds one workgroup of >= 768 threads (768 / blk of smaller ones); 2 KB below the
+    // threads per workgroup, and traversal stacks per workgroup (one per path: two per thread in
+    // yk_render_dual)
+    const int blk = v == 2 ? kDualBlock : block_of(v == 1);
+    const int rays = v == 2 ? kDualRays : blk;
+    // a CU holds one workgroup of >= 512 threads (768 / blk of smaller ones); 2 KB below the
     // share: the hardware's allocation granularity (3 blocks of 54144 bytes measured only 2
     // resident per CU)
-    const size_t budget = (size_t)160 * 1024 / (blk >= 768 ? 1 : 768 / blk) - 2048;
-    const size_t min_stacks = (size_t)12 * blk * 4;
+    const size_t budget = (size_t)160 * 1024 / (blk >= 512 ? 1 : 768 / blk) - 2048;
+    const size_t min_stacks = (size_t)12 * rays * 4;
     pl.in_lds = scene_bytes + tgeo_bytes + mat_bytes + min_stacks <= budget;
     const size_t tables = pl.in_lds ? tgeo_bytes + mat_bytes : 0;
     // Traversal stack per lane: up to 3 pushes per wide level suffice (3 * wdepth + 1 entries);
@@ -2382,14 +2491,14 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
     // current top (up to 3 past the capacity): +4 entries.
     {
       const size_t used = pl.in_lds ? scene_bytes + tables : 0;
-      const uint32_t fit = used + min_stacks <= budget ? (uint32_t)((budget - used) / (blk * 4)) : 12u;
+      const uint32_t fit = used + min_stacks <= budget ? (uint32_t)((budget - used) / (rays * 4)) : 12u;
       pl.stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
       pl.stack_entries = pl.stack_cap + 4;
     }
     pl.tgeo_off = pl.in_lds && tgeo_elem ? (uint32_t)scene_bytes : 0u;
     pl.mat_off = pl.in_lds && tgeo_elem ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
     pl.stack_off = pl.in_lds ? (uint32_t)(scene_bytes + tables) : 0u;
-    pl.lds_bytes = pl.stack_off + pl.stack_entries * blk * (uint32_t)sizeof(int32_t);
+    pl.lds_bytes = pl.stack_off + pl.stack_entries * rays * (uint32_t)sizeof(int32_t);
     int per_cu = 0;
     const RenderKernel k = kern[v][pl.in_lds ? 1 : 0];
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, blk, pl.lds_bytes);
@@ -2440,6 +2549,9 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   for (int k8 = 0; k8 < 8; ++k8)
     (void)hipFuncSetAttribute((const void*)f32_kernel(k8 & 4, (k8 & 1) | ((k8 & 2) << 1)),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int k8 = 0; k8 < 8; ++k8)
+    (void)hipFuncSetAttribute((const void*)dual_kernel(k8 & 4, k8 & 3), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
@@ -2498,7 +2610,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
     // sphere<float>: centre and radius rounded to float, radius*radius a float product
     const float rf = (float)s.radius;
     geo_f[i] = make_float4((float)s.center[0], (float)s.center[1], (float)s.center[2], rf * rf);
-    mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0u, 0.0};  // inv_r: yk_mat_prep
+    mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0.0f, 0.0};  // inv_r*: yk_mat_prep
   }
   YK_HIP(hipSetDevice(ctx->device));
   // a render enqueued by ykgpu_render_async on the caller's stream (and its launches on the
@@ -2542,8 +2654,9 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   // SAH over all three axes: 512-spp A/B 199.4 -> 198.3 ms (model: 5.51 -> 5.13 visits per segment)
   bopt.all_axes = true;
   if (const char* e = std::getenv("YKGPU_BVH_ALLAXES")) bopt.all_axes = std::atoi(e) != 0;                  // (A/B)
-  const RenderKernel k64[2][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
-                                  {fp64_kernel(false, 4), fp64_kernel(true, 4)}};
+  const RenderKernel k64[3][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
+                                  {fp64_kernel(false, 4), fp64_kernel(true, 4)},
+                                  {dual_kernel(false, 0), dual_kernel(true, 0)}};
   int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, kLeafCapF64, geo.data(), sizeof(SphereGeo),
                        sizeof(SphereGeo), k64);
   if (rc) return rc;
@@ -2552,8 +2665,9 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   if (const char* e = std::getenv("YKGPU_BVH_ALLAXES_F32")) fopt.all_axes = std::atoi(e) != 0;  // (A/B; on: neutral)
   fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
   fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
-  const RenderKernel k32[2][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
-                                  {f32_kernel(false, 4), f32_kernel(true, 4)}};
+  const RenderKernel k32[3][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
+                                  {f32_kernel(false, 4), f32_kernel(true, 4)},
+                                  {f32_kernel(false, 0), f32_kernel(true, 0)}};  // (no dual FP32 kernel)
   rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, kLeafCapF32, geo_f.data(), sizeof(float4),
                    sizeof(float4), k32);
   if (rc) return rc;
@@ -2708,6 +2822,26 @@ int ykgpu_math_div(ykgpu_context* ctx, const double* num3, const double* den, do
   if (e == hipSuccess) e = hipMemcpy(out3, d + 4 * n, 3 * n * sizeof(double), hipMemcpyDeviceToHost);
   (void)hipFree(d);
   if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_math_div: ") + hipGetErrorString(e));
+  return YK_OK;
+}
+
+int ykgpu_math_div_f32(ykgpu_context* ctx, const float* num3, const float* den, float* out3, uint64_t n) {
+  if (!ctx || (n && (!num3 || !den || !out3))) return fail(YK_ERR_INVALID, "null argument");
+  if (n == 0) return YK_OK;
+  YK_HIP(hipSetDevice(ctx->device));
+  float* d = nullptr;
+  YK_HIP(hipMalloc(&d, 7 * n * sizeof(float)));
+  hipError_t e = hipMemcpy(d, num3, 3 * n * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d + 3 * n, den, n * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(yk_math_div_f32, dim3((uint32_t)blocks), dim3(256), 0, ctx->stream, d, d + 3 * n, d + 4 * n, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipMemcpy(out3, d + 4 * n, 3 * n * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(YK_ERR_DEVICE, std::string("ykgpu_math_div_f32: ") + hipGetErrorString(e));
   return YK_OK;
 }
 
