@@ -184,6 +184,8 @@ typedef struct yk_render_stats {
                               back when it needs less than half                            */
   uint64_t call_bytes;     /* device memory THIS call needed (the same items sized to it):
                               1920x1080x512 FP64 ~13.7 GB; a 270-row tile of 3840 ~7.4 GB   */
+  double sclk_mhz;         /* the shader clock the render launches ran at: s_memtime over
+                              s_memrealtime (100 MHz) of one wave per launch, averaged      */
 } yk_render_stats;
 
 typedef struct ykgpu_context ykgpu_context;

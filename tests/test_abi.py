@@ -103,11 +103,12 @@ def test_group_invalid_arguments_are_reported():
 
 
 def test_render_stats_layout_matches_the_header():
-    """yk_render_stats ends with device_bytes at offset 312 and call_bytes at 320 (include/ykgpu.h,
-    ABI 9)."""
+    """yk_render_stats ends with device_bytes at offset 312, call_bytes at 320 and sclk_mhz at 328
+    (include/ykgpu.h, ABI 9)."""
     assert records.RenderStats.device_bytes.offset == 312
     assert records.RenderStats.call_bytes.offset == 320
-    assert ctypes.sizeof(records.RenderStats) == 328
+    assert records.RenderStats.sclk_mhz.offset == 328
+    assert ctypes.sizeof(records.RenderStats) == 336
 
 
 def test_invalid_arguments_are_reported():

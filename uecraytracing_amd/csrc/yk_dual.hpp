@@ -460,6 +460,7 @@ void yk_render_dual(KernelArgs ka) {
 #if YK_RENDER_PRIO
   __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);
 #endif
+  YK_CLOCK_BEGIN(ka);
 
   DPath<Gen> A, B;
   rng_init(A.g, ka, 2 * gid);
@@ -583,6 +584,7 @@ void yk_render_dual(KernelArgs ka) {
     dual_shade_end<kCount>(ka, B, aliveB, hB, geo, mat, n_ncall, n_nit, n_fb, n_lamb, n_metal, n_fuzz, n_diel);
   }
 
+  YK_CLOCK_END(ka);
   if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
     atomicAdd(&ka.counters[1], (unsigned long long)n_test);

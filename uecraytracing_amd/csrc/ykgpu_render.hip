@@ -170,7 +170,22 @@ struct KernelArgs {
   double* trace;                 // YK_FLAG_TRACE_RAYS: rays [(q*spp + s)*trace_cap + k][6]
   uint32_t* trace_counts;        //   ray_color calls per sample [q*spp + s]
   uint32_t trace_cap, pad_t;
+  unsigned long long* clk;  // this launch's shader-clock probe (YK_CLOCK_*): 4 words
 };
+
+// Shader-clock probe of a launch: thread 0 of block 0 stores s_memtime (the shader clock) and
+// s_memrealtime (100 MHz) when it starts and when it leaves the loop (vector stores, nothing held
+// in registers across the loop) — the clock the launch ran at (ykgpu_get_stats sclk_mhz; the
+// per-launch timeline).
+#define YK_CLOCK_STAMP(ka, k)                                                              \
+  do {                                                                                     \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                             \
+      (ka).clk[(k)] = __builtin_amdgcn_s_memtime();                                        \
+      (ka).clk[(k) + 1] = __builtin_amdgcn_s_memrealtime();                                \
+    }                                                                                      \
+  } while (0)
+#define YK_CLOCK_BEGIN(ka) YK_CLOCK_STAMP(ka, 0)
+#define YK_CLOCK_END(ka) YK_CLOCK_STAMP(ka, 2)
 
 // -l 3 (raytracer.hpp:21-25): ray k of the path of the lane's sample slot (counting instance)
 template <class V>
@@ -578,6 +593,16 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
   return !in_path && slot >= ka.nsl;
 }
 
+using RenderKernel = void (*)(KernelArgs);
+
+// YK_SPLIT (Makefile): 0 — every kernel in this translation unit (the A/B variants of
+// tools/build_def_variant.sh); 1 — the library's main unit, without the FP32 render kernel; 2 —
+// the FP32 render kernel alone, compiled under LLVM's max-ilp scheduler (FP32 512 spp: -1.3%;
+// the same scheduler costs the FP64 kernel +1.5%)
+#ifndef YK_SPLIT
+#define YK_SPLIT 0
+#endif
+#if YK_SPLIT != 2
 // kCount: the work counters of YK_FLAG_COUNT_WORK (an instance of its own, so the production
 // instance carries neither their registers nor their adds)
 // kMode bit 0: the work counters; bit 1: YK_SEED_RANDOM_DEVICE seeding (an instance of its own:
@@ -636,6 +661,7 @@ void yk_render_persistent(KernelArgs ka) {
   // the warm-up waves sharing the SIMDs (priority 0) get only the issue slots the render leaves
   __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);
 #endif
+  YK_CLOCK_BEGIN(ka);
 
   Gen g;
   rng_init(g, ka, gid);
@@ -1131,6 +1157,7 @@ void yk_render_persistent(KernelArgs ka) {
     YK_STAMP(5);
   }
 
+  YK_CLOCK_END(ka);
   YK_STAMPS_END(ka.counters, lane);
   if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
@@ -1150,7 +1177,6 @@ void yk_render_persistent(KernelArgs ka) {
 }
 
 // The FP64 instance for (scene in LDS, kMode)
-using RenderKernel = void (*)(KernelArgs);
 RenderKernel fp64_kernel(bool lds, int mode) {
   static const RenderKernel k[16] = {
       yk_render_persistent<false, 0>, yk_render_persistent<false, 1>, yk_render_persistent<false, 2>,
@@ -1163,6 +1189,9 @@ RenderKernel fp64_kernel(bool lds, int mode) {
 }
 
 #include "yk_dual.hpp"
+#endif  // YK_SPLIT != 2
+
+#if YK_SPLIT != 1
 
 // ---- render<float> (YK_PRECISION_FP32) ---------------------------------------------------
 // The same persistent, sample-parallel structure as yk_render_persistent (refill, slots, start
@@ -1289,6 +1318,7 @@ void yk_render_f32(KernelArgs ka) {
 #if YK_RENDER_PRIO
   __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);  // over the co-resident warm-up waves, as in FP64
 #endif
+  YK_CLOCK_BEGIN(ka);
   Gen g;
   rng_init(g, ka, gid);
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
@@ -1735,6 +1765,7 @@ void yk_render_f32(KernelArgs ka) {
     }
     YK_STAMP(5);
   }
+  YK_CLOCK_END(ka);
   YK_STAMPS_END(ka.counters, lane);
   if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
@@ -1756,6 +1787,8 @@ RenderKernel f32_kernel(bool lds, int mode) {
   return k[(lds ? 4 : 0) + ((mode & 1) | ((mode & 4) >> 1))];
 }
 
+#endif  // YK_SPLIT != 1
+
 // ykgpu_math_sqrt_f32: the FP32 path's math::sqrt<float> on a buffer (diagnostic).
 __global__ __launch_bounds__(256) void yk_math_sqrt_f32(const float* in, float* out, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1764,6 +1797,17 @@ __global__ __launch_bounds__(256) void yk_math_sqrt_f32(const float* in, float* 
 }
 
 }  // namespace
+
+#if YK_SPLIT == 2
+// the FP32 unit's instances, for the main unit's f32_kernel()
+extern "C" const void* yk_split_f32_kernel(bool lds, int mode) { return (const void*)f32_kernel(lds, mode); }
+#else
+#if YK_SPLIT == 1
+extern "C" const void* yk_split_f32_kernel(bool lds, int mode);  // ykgpu_render_f32.o
+namespace {
+RenderKernel f32_kernel(bool lds, int mode) { return (RenderKernel)yk_split_f32_kernel(lds, mode); }
+}  // namespace
+#endif
 
 // =========================================================================================
 // C-ABI
@@ -1827,6 +1871,7 @@ struct ykgpu_context {
   bool have_scene = false;
   uint32_t* d_counter = nullptr;        // sample-slot counters, one per launch of a call
   uint32_t counter_cap = 0;
+  unsigned long long* d_clk = nullptr;  // shader-clock probes, 4 words per launch (YK_CLOCK_*)
   unsigned long long* d_stats = nullptr;  // kCounters counters
   uint32_t* d_mt = nullptr;            // grid*256*624 words
   uint16_t* d_ids = nullptr;            // grid*256*id_stride
@@ -2240,9 +2285,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // that waits for a free CU behind the warm-ups and reduces (up to 1.6 ms per launch, measured)
   if (nlaunch > ctx->counter_cap) {
     (void)hipFree(ctx->d_counter);
+    (void)hipFree(ctx->d_clk);
     ctx->d_counter = nullptr;
+    ctx->d_clk = nullptr;
     ctx->counter_cap = 0;
     YK_HIP(hipMalloc(&ctx->d_counter, nlaunch * sizeof(uint32_t)));
+    YK_HIP(hipMalloc(&ctx->d_clk, 4ull * nlaunch * sizeof(unsigned long long)));
     ctx->counter_cap = nlaunch;
   }
   YK_HIP(hipMemsetAsync(ctx->d_counter, 0, nlaunch * sizeof(uint32_t), st));
@@ -2308,6 +2356,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its start records
     if (c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
     ka.pixel_counter = ctx->d_counter + c;
+    ka.clk = ctx->d_clk + 4 * c;
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (f32)
@@ -2403,12 +2452,28 @@ int finish_stats(ykgpu_context* ctx) {
     busy += b - std::min<double>(b, std::max<double>(0.0, ov));
   }
   ctx->stats.render_busy_ms = busy;
+  // the shader clock of each launch (YK_CLOCK_* probe: wave 0 of block 0), averaged over the call
+  // weighted by the probe's real time
+  const uint32_t nl = ctx->lev_used / 6;
+  std::vector<unsigned long long> clk(4ull * nl);
+  std::vector<double> mhz(nl, 0.0);
+  if (nl) YK_HIP(hipMemcpy(clk.data(), ctx->d_clk, clk.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  double cyc = 0, real = 0;
+  for (uint32_t k = 0; k < nl; ++k) {
+    const double dc = (double)(clk[4 * k + 2] - clk[4 * k]), dr = (double)(clk[4 * k + 3] - clk[4 * k + 1]);
+    if (dr > 0 && clk[4 * k + 3] > clk[4 * k + 1]) {
+      mhz[k] = dc / dr * 100.0;  // s_memrealtime ticks at 100 MHz
+      cyc += dc;
+      real += dr;
+    }
+  }
+  ctx->stats.sclk_mhz = real > 0 ? cyc / real * 100.0 : 0.0;
   if (std::getenv("YKGPU_TIMELINE")) {  // diagnostic: per-launch event times (ms from the call's start)
     for (uint32_t k = 0; k + 5 < ctx->lev_used; k += 6) {
       float t[6];
       for (int q = 0; q < 6; ++q) YK_HIP(hipEventElapsedTime(&t[q], ctx->ev0, ctx->lev[k + q]));
-      std::fprintf(stderr, "launch %u: warm %8.3f %8.3f  render %8.3f %8.3f  reduce %8.3f %8.3f\n", k / 6, t[0], t[1],
-                   t[2], t[3], t[4], t[5]);
+      std::fprintf(stderr, "launch %u: warm %8.3f %8.3f  render %8.3f %8.3f  reduce %8.3f %8.3f  sclk %7.1f MHz\n",
+                   k / 6, t[0], t[1], t[2], t[3], t[4], t[5], mhz[k / 6]);
     }
     std::fprintf(stderr, "call %8.3f\n", ms);
   }
@@ -2573,6 +2638,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_mat);
   (void)hipFree(ctx->d_geo_f);
   (void)hipFree(ctx->d_counter);
+  (void)hipFree(ctx->d_clk);
   (void)hipFree(ctx->d_stats);
   (void)hipFree(ctx->d_warm);
   (void)hipFree(ctx->d_order);
@@ -2982,6 +3048,7 @@ int ykgpu_group_render(ykgpu_group* g, const yk_render_params* p, uint8_t* rgb_h
     tot.seed_key = s.seed_key;
     tot.device_bytes += s.device_bytes + g->tile_cap[e];
     tot.call_bytes += s.call_bytes + rows[e] * row_bytes;
+    tot.sclk_mhz = std::max(tot.sclk_mhz, s.sclk_mhz);
   }
   tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   g->total = tot;
@@ -3014,3 +3081,4 @@ int ykgpu_render_devices(const int* devices, uint32_t n_devices, const yk_sphere
 }
 
 }  // extern "C"
+#endif  // YK_SPLIT != 2

@@ -114,6 +114,7 @@ class RenderStats(ctypes.Structure):
         ("work", ctypes.c_uint64 * 8),
         ("device_bytes", ctypes.c_uint64),
         ("call_bytes", ctypes.c_uint64),
+        ("sclk_mhz", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -128,7 +129,7 @@ class RenderStats(ctypes.Structure):
 assert ctypes.sizeof(Sphere) == 80
 assert ctypes.sizeof(Camera) == 19 * 8
 assert ctypes.sizeof(RenderParams) == 72
-assert ctypes.sizeof(RenderStats) == 328
+assert ctypes.sizeof(RenderStats) == 336
 
 
 def image_height_for(width: int) -> int:
