@@ -15,7 +15,7 @@ for rnd in 0 1; do
     if [ $v = base ]; then L=$PWD/uecraytracing_amd/lib/libykgpu.so; else L=$PWD/uecraytracing_amd/lib/abl/libykgpu_$v.so; fi
     envs=("YKGPU_LIB_OVERRIDE=$L")
     for e in "${parts[@]:1}"; do envs+=("$e"); done
-    env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-modes > gpurun_out/$T/bench_${i}_$rnd.log 2>&1 || { echo BENCH_FAILED $spec; tail -5 gpurun_out/$T/bench_${i}_$rnd.log; exit 1; }
+    env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-modes --no-configs --no-tiles > gpurun_out/$T/bench_${i}_$rnd.log 2>&1 || { echo BENCH_FAILED $spec; tail -5 gpurun_out/$T/bench_${i}_$rnd.log; exit 1; }
     python3 -c "
 import json
 d=json.loads([l for l in open('gpurun_out/$T/bench_${i}_$rnd.log') if l.startswith('{')][-1])

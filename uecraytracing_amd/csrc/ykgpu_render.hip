@@ -385,6 +385,7 @@ struct WarmArgs {
   const uint32_t* order;
   uint64_t n;  // sample slots in the launch
   void* out;
+  uint32_t* counter;  // the launch's sample-slot counter: cleared here (the render waits for this kernel)
 };
 
 template <bool kLens, bool kF32>
@@ -392,6 +393,7 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
   // (32-bit indices: a launch keeps its slots below 2^31 and the grid below 2^21 threads)
   const uint32_t n = (uint32_t)wa.n;
   const uint32_t stride = gridDim.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *wa.counter = 0u;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
     const uint32_t q = wa.order[pp];
@@ -1863,6 +1865,16 @@ struct ykgpu_context {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> lev;  // per launch: warm-up start, render start, reduce start, end
   uint32_t lev_used = 0;
+  // Cross-call pipelining (launch()): the previous call's per-launch events and ring geometry, and
+  // a global launch counter that numbers the ring slots, the scratch parity and the render
+  // stream across calls
+  std::vector<hipEvent_t> lev_prev;
+  uint32_t prev_n = 0, prev_R = 0, prev_CR = 0;
+  uint64_t prev_geom = 0;  // hash of (slots per launch buffer, record size, ring buffers)
+  bool prev_ok = false;
+  bool prev_enqueued = false;  // the previous call's launches were all enqueued (its events exist)
+  bool dirty = false;          // a call failed part-way: its enqueued work is not tracked
+  uint64_t g_next = 0;
   SphereGeo* d_geo = nullptr;
   SphereMat* d_mat = nullptr;
   float4* d_geo_f = nullptr;  // FP32 geometry (cx, cy, cz, r*r in float), tuple order
@@ -1937,9 +1949,18 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
   return YK_OK;
 }
 
+// Waits for every stream of the context: before a buffer that an earlier call's kernels may still
+// use is freed (with cross-call pipelining a call's first launches run beside the previous call's
+// last ones, launch())
+int quiesce(ykgpu_context* ctx) {
+  for (hipStream_t s : {ctx->aux, ctx->red, ctx->ren, ctx->alt, ctx->stream}) YK_HIP(hipStreamSynchronize(s));
+  return YK_OK;
+}
+
 int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, size_t lanes, bool need_mt) {
   // mt19937 fallback engines: 624 words per persistent lane (not needed by xor128)
   if (need_mt && (lanes > ctx->scratch_lanes || !ctx->d_mt)) {
+    if (int rc = quiesce(ctx)) return rc;
     (void)hipFree(ctx->d_mt);
     ctx->d_mt = nullptr;
     ctx->scratch_lanes = 0;
@@ -1949,6 +1970,7 @@ int ensure_scratch(ykgpu_context* ctx, uint32_t max_depth, size_t lanes, bool ne
   // attenuation-id spill: max_depth u16 per lane
   const uint32_t need = max_depth > kStackRegs ? max_depth : 1;
   if (need > ctx->id_stride || lanes > ctx->id_lanes || !ctx->d_ids) {
+    if (int rc = quiesce(ctx)) return rc;
     if (ctx->d_ids) YK_HIP(hipFree(ctx->d_ids));
     ctx->d_ids = nullptr;
     ctx->id_stride = 0;
@@ -2029,6 +2051,7 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride)
           ord.push_back(x < W && y < rows ? y * W + x : kNoPixel);
         }
   }
+  if (int rc = quiesce(ctx)) return rc;
   (void)hipFree(ctx->d_order);
   ctx->d_order = nullptr;
   ctx->order_w = ctx->order_rows = ctx->order_slots = 0;
@@ -2140,7 +2163,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
                              std::max<uint64_t>({kLaunchSpp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
-  for (uint32_t s0 = 0, k = std::min(kFirstLaunch, kmax); s0 < spp;) {
+  // (A/B knobs: YKGPU_FIRST_LAUNCH, YKGPU_SCHED_GROW — the first launch's samples per pixel and
+  // the factor each next launch grows by until kmax)
+  uint32_t first_k = kFirstLaunch, grow_k = 4;
+  if (const char* e = std::getenv("YKGPU_FIRST_LAUNCH")) first_k = (uint32_t)std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("YKGPU_SCHED_GROW")) grow_k = (uint32_t)std::max(2, std::atoi(e));
+  for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
     uint32_t take = std::min(k, spp - s0);
     const uint32_t rest = spp - (s0 + take);
     if (rest > 0 && rest < std::max(1u, take / 4)) {
@@ -2150,7 +2178,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     }
     sched.emplace_back(s0, take);
     s0 += take;
-    k = std::min(4 * k, kmax);
+    k = std::min(grow_k * k, kmax);
   }
   uint32_t K = 0;  // largest launch
   for (auto& l : sched) K = std::max(K, l.second);
@@ -2158,6 +2186,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // less than half of it (device_bytes then reports about what the call holds)
   auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t elem) -> int {
     if (need <= cap && 2 * need >= cap) return YK_OK;
+    if (int q = quiesce(ctx)) return q;
     (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
@@ -2281,41 +2310,80 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ra.npix_slots = nps;
   ra.spp = spp;
   ra.pad0 = ra.pad1 = 0;
-  // one slot counter per launch, all cleared here: a clear between launches is a fill kernel
-  // that waits for a free CU behind the warm-ups and reduces (up to 1.6 ms per launch, measured)
-  if (nlaunch > ctx->counter_cap) {
+  // Cross-call pipelining: the launches are numbered across calls (ctx->g_next) and a launch's
+  // ring slots (start records, colours, slot counter), scratch parity and render stream follow its
+  // global number, so a call whose rings have the previous call's geometry needs no barrier
+  // behind it: its warm-up c (c < ring) waits only for the previous call's render that last read
+  // that start-record buffer, its render c only for the reduce that last read that colour
+  // buffer, and only its last reduce, which writes the caller's image, waits for the caller's
+  // stream (ev0).  Back-to-back calls then overlap like the launches inside a call: the next
+  // call's first warm-up and renders take the CUs the last launch's draining blocks free.
+  // YKGPU_OVERLAP=0 (A/B) keeps every call behind the caller's stream, as do xor128 calls (no
+  // warm-up kernel to clear their slot counters) and any call after a failed one.
+  const uint64_t g0 = ctx->g_next;
+  const uint64_t geom = ((uint64_t)nps * K * welem) ^ ((uint64_t)(uintptr_t)ctx->d_warm << 1) ^
+                        ((uint64_t)(uintptr_t)ctx->d_col << 2) ^ ((uint64_t)kWarmRing << 56) ^ ((uint64_t)kColRing << 60);
+  const char* ove = std::getenv("YKGPU_OVERLAP");
+  const bool ov = !x128 && !warm_first && !(ove && std::atoi(ove) == 0) && ctx->prev_ok && ctx->prev_geom == geom &&
+                  ctx->prev_R == kWarmRing && ctx->prev_CR == kColRing && ctx->prev_n >= std::max(kWarmRing, kColRing);
+  if (ctx->dirty && (rc = quiesce(ctx))) return rc;  // a failed call's work: wait it out on the host
+  const bool after_prev = ctx->prev_enqueued && !ctx->dirty && !ov;
+  ctx->prev_ok = false;  // (until this call has been enqueued)
+  ctx->dirty = true;
+  // slot counters: one per launch of the call for xor128 (cleared here), one per start-record
+  // buffer for mt19937 (cleared by the launch's warm-up kernel: a clear between launches as a
+  // fill kernel of its own would wait for a free CU behind the warm-ups and reduces, up to 1.6 ms
+  // per launch, measured)
+  if (std::max(nlaunch, kWarmRing) > ctx->counter_cap) {
+    if ((rc = quiesce(ctx))) return rc;
     (void)hipFree(ctx->d_counter);
     (void)hipFree(ctx->d_clk);
     ctx->d_counter = nullptr;
     ctx->d_clk = nullptr;
     ctx->counter_cap = 0;
-    YK_HIP(hipMalloc(&ctx->d_counter, nlaunch * sizeof(uint32_t)));
-    YK_HIP(hipMalloc(&ctx->d_clk, 4ull * nlaunch * sizeof(unsigned long long)));
-    ctx->counter_cap = nlaunch;
+    YK_HIP(hipMalloc(&ctx->d_counter, std::max(nlaunch, kWarmRing) * sizeof(uint32_t)));
+    YK_HIP(hipMalloc(&ctx->d_clk, 4ull * std::max(nlaunch, kWarmRing) * sizeof(unsigned long long)));
+    ctx->counter_cap = std::max(nlaunch, kWarmRing);
   }
-  YK_HIP(hipMemsetAsync(ctx->d_counter, 0, nlaunch * sizeof(uint32_t), st));
-  YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
-  YK_HIP(hipMemsetAsync(ctx->d_stats + 16, 0xff, 2 * sizeof(unsigned long long), st));  // minima
-  YK_HIP(hipEventRecord(ctx->ev0, st));
-  YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->ev0, 0));  // the caller's earlier work comes first
   // per launch: [0] warm-up start, [1] warm-up end (aux), [2] render start, [3] render end (st),
-  // [4] reduce start, [5] reduce end (red)
+  // [4] reduce start, [5] reduce end (red); the previous call's stay in lev_prev
+  std::swap(ctx->lev, ctx->lev_prev);
   while (ctx->lev.size() < 6ull * nlaunch) {
     hipEvent_t e;
     YK_HIP(hipEventCreate(&e));
     ctx->lev.push_back(e);
   }
   ctx->lev_used = 6 * nlaunch;
-  YK_HIP(hipStreamWaitEvent(ctx->red, ctx->ev0, 0));
-  YK_HIP(hipStreamWaitEvent(ctx->alt, ctx->ev0, 0));
-  YK_HIP(hipStreamWaitEvent(ctx->ren, ctx->ev0, 0));
+  if (x128) YK_HIP(hipMemsetAsync(ctx->d_counter, 0, nlaunch * sizeof(uint32_t), st));
+  if (!ov) {
+    YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
+    YK_HIP(hipMemsetAsync(ctx->d_stats + 16, 0xff, 2 * sizeof(unsigned long long), st));  // minima
+  }
+  YK_HIP(hipEventRecord(ctx->ev0, st));
+  if (ov) {
+    // (the previous call's last renders may still add their MT-fallback counts here)
+    YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), ctx->aux));
+    YK_HIP(hipMemsetAsync(ctx->d_stats + 16, 0xff, 2 * sizeof(unsigned long long), ctx->aux));
+  } else {
+    // the caller's earlier work, and the whole previous call (its last reduce ends after every
+    // launch of it: whichever stream the caller used then), come first
+    for (hipStream_t s : {ctx->aux, ctx->red, ctx->alt, ctx->ren}) {
+      YK_HIP(hipStreamWaitEvent(s, ctx->ev0, 0));
+      if (after_prev) YK_HIP(hipStreamWaitEvent(s, ctx->lev_prev[6 * (ctx->prev_n - 1) + 5], 0));
+    }
+  }
+  const uint32_t pn = ctx->prev_n;
   auto warm = [&](uint32_t c) -> int {
     hipEvent_t* ev = &ctx->lev[6 * c];
-    // its buffer: the render of launch c - ring has read its records
-    if (c >= kWarmRing) YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
+    // its buffer: the render that last read it (launch c - ring, possibly the previous call's)
+    if (c >= kWarmRing)
+      YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
+    else if (ov)
+      YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev_prev[6 * (pn - kWarmRing + c) + 3], 0));
     wa.s0 = sched[c].first;
     wa.n = (uint64_t)nps * sched[c].second;
-    wa.out = ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
+    wa.out = ctx->d_warm + (size_t)((g0 + c) % kWarmRing) * nps * K * welem;
+    wa.counter = ctx->d_counter + (g0 + c) % kWarmRing;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * warm_per_cu(f32));
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
@@ -2340,8 +2408,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     hipEvent_t* ev = &ctx->lev[6 * c];
     const uint32_t s0 = sched[c].first, ks = sched[c].second;
     const uint32_t nsl = nps * ks;
-    char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(c % kWarmRing) * nps * K * welem;
-    double* col = ctx->d_col + (size_t)(c % kColRing) * nps * K * kColStride;
+    const uint64_t g = g0 + c;  // the launch's global number (ring slots, parity, stream)
+    char* const wring = x128 ? nullptr : ctx->d_warm + (size_t)(g % kWarmRing) * nps * K * welem;
+    double* col = ctx->d_col + (size_t)(g % kColRing) * nps * K * kColStride;
     ka.s0 = s0;
     ka.nsl = nsl;
     ka.col = col;
@@ -2349,13 +2418,17 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     // Render launches alternate between the caller's stream and ctx->alt: launch c + 1 depends
     // only on its own start records and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
-    const hipStream_t rs = (c & 1) ? ctx->alt : ctx->ren;
+    const hipStream_t rs = (g & 1) ? ctx->alt : ctx->ren;
     const size_t lanes = (size_t)grid * block * paths;
-    ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (c & 1) * lanes * ykd::kMtN : nullptr;
-    ka.id_scratch = ctx->d_ids + (c & 1) * lanes * ctx->id_stride;
-    YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));                                // its start records
-    if (c >= kColRing) YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));  // its colour buffer
-    ka.pixel_counter = ctx->d_counter + c;
+    ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (g & 1) * lanes * ykd::kMtN : nullptr;
+    ka.id_scratch = ctx->d_ids + (g & 1) * lanes * ctx->id_stride;
+    YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));  // its start records
+    // its colour buffer: the reduce that last read it
+    if (c >= kColRing)
+      YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));
+    else if (ov)
+      YK_HIP(hipStreamWaitEvent(rs, ctx->lev_prev[6 * (pn - kColRing + c) + 5], 0));
+    ka.pixel_counter = ctx->d_counter + (x128 ? c : (uint32_t)(g % kWarmRing));
     ka.clk = ctx->d_clk + 4 * c;
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
@@ -2377,6 +2450,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ra.first = s0 == 0;
     ra.last = s0 + ks == spp;
     YK_HIP(hipStreamWaitEvent(ctx->red, ev[3], 0));
+    if (ov && ra.last) YK_HIP(hipStreamWaitEvent(ctx->red, ctx->ev0, 0));  // the caller's image
     YK_HIP(hipEventRecord(ev[4], ctx->red));
     hipLaunchKernelGGL(yk_reduce_samples, dim3(reduce_blocks(ctx, nps)), dim3(256), 0, ctx->red, ra);
     YK_HIP(hipGetLastError());
@@ -2386,6 +2460,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   }
   YK_HIP(hipStreamWaitEvent(st, ctx->lev[6 * (nlaunch - 1) + 5], 0));  // the caller sees the image
   YK_HIP(hipEventRecord(ctx->ev1, st));
+  ctx->g_next = g0 + nlaunch;
+  ctx->prev_n = nlaunch;
+  ctx->prev_R = kWarmRing;
+  ctx->prev_CR = kColRing;
+  ctx->prev_geom = geom;
+  ctx->prev_ok = !x128 && !warm_first;
+  ctx->prev_enqueued = true;
+  ctx->dirty = false;
   ctx->stats = yk_render_stats{};
   ctx->stats.samples = (uint64_t)p->row_count * p->image_width * p->samples_per_pixel;
   ctx->stats.launches = launches;
@@ -2651,6 +2733,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_rgb);
   (void)hipFree(ctx->d_sums);
   for (hipEvent_t e : ctx->lev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->lev_prev) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
