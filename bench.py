@@ -159,28 +159,31 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf):
 
 def rank_tiles(ren, stream, seed0, frame_ms):
     """The N-GPU bound on this GPU: every rank's row tile of the N-way
-    split rendered ALONE (best of two calls, HIP events on the bench stream), for config 3 at
-    N = 2, 4, 8 and config 4's eight 270-row tiles.  The slowest tile bounds the N-GPU step before
-    the gather; `speedup_bound` = the single-GPU call (frame_ms, config 3; one timed config-4
-    frame otherwise) / the slowest tile."""
+    split rendered ALONE (ms per call over 4 back-to-back calls after a warm one, HIP events on the
+    bench stream: the per-rank steps of the N-GPU bench), for config 3 at N = 2, 4, 8 and config 4's
+    eight 270-row tiles.  The slowest tile bounds the N-GPU step before the gather;
+    `speedup_bound` = the single-GPU frame (the contract line's ms per step for config 3; the
+    same back-to-back timing of whole config-4 frames) / the slowest tile."""
     import torch
 
     import uecraytracing_amd as yk
     from uecraytracing_amd.records import image_height_for, make_params
     from uecraytracing_amd.tiles import tile_rows
 
-    def call_ms(p, out):
-        best = None
-        for _ in range(2):
-            with torch.cuda.stream(stream):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
+    def call_ms(p, out, calls=4):
+        # one warm call, then `calls` back-to-back calls as the N-GPU bench's steps issue them (a
+        # call's first launches overlap the previous call's last, DESIGN §3): ms per call
+        with torch.cuda.stream(stream):
+            ren.render_async(p, out.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(stream):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(calls):
                 ren.render_async(p, out.data_ptr(), stream.cuda_stream)
-                e1.record(stream)
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1)
-            best = ms if best is None else min(best, ms)
-        return best
+            e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / calls
 
     out = {}
     for cfg, W, spp, ns in (("config3", 1920, 512, (2, 4, 8)), ("config4", 3840, 1024, (8,))):
@@ -507,7 +510,7 @@ def main():
         result["configs"] = other_configs(ren, stream, args.seed0, args.cpu_threads or usable_cpus()[0], peak_tf)
 
     if rank == 0 and world == 1 and not args.no_tiles and (W, spp, depth, args.scene) == (1920, 512, 50, "final"):
-        result["tiles"] = rank_tiles(ren, stream, args.seed0, call_ms)
+        result["tiles"] = rank_tiles(ren, stream, args.seed0, ms_per_step)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -107,9 +107,12 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #ifndef YK_RENDER_PRIO
 #define YK_RENDER_PRIO 1
 #endif
-// the FP64 visit's slab constants as one op_sel-read register pair per axis and bound (yk_slab.hpp)
+// the visit's slab constants as one op_sel-read register pair per axis and bound (yk_slab.hpp):
+// 123 -> 115 VGPRs (FP64), 125 -> 111 (FP32), but no faster (512 spp: FP64 173.9 -> 174.1 ms,
+// FP32 194.2 -> 195.2 ms, profiles/r04_ab/); the one-path kernels keep the broadcast pairs,
+// yk_render_dual (which needs the registers) uses them always
 #ifndef YK_SLAB_PAIRS
-#define YK_SLAB_PAIRS 1
+#define YK_SLAB_PAIRS 0
 #endif
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
@@ -2017,9 +2020,18 @@ constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
 #endif
 constexpr uint32_t kWarmRingDepth = YK_WARM_RING;
 #ifndef YK_FIRST_LAUNCH
-#define YK_FIRST_LAUNCH 8
+#define YK_FIRST_LAUNCH 4
 #endif
 constexpr uint32_t kFirstLaunch = YK_FIRST_LAUNCH;  // samples per pixel in the first launch
+// ... and each next launch grows by this factor until kmax: 4, 8, 16, 32, 32, ... (1920x1080x512:
+// 4 + 8 + 16 + 14 x 32 + 18 + 18 = 512 spp in 19 launches).  Before round 4: 8, 32, 32, ...; its second
+// warm-up (32 spp of walks beside the first render) sometimes finished late and delayed every
+// launch after it: 20 synced calls on one box spread 173.6-177.4 ms (max/min 1.022), against
+// 173.6-174.6 (1.0059) with 4, 8, 16 (tools/variance_ab.py, profiles/r04_ab/variance/)
+#ifndef YK_SCHED_GROW
+#define YK_SCHED_GROW 2
+#endif
+constexpr uint32_t kSchedGrow = YK_SCHED_GROW;
 static_assert(YK_FIRST_LAUNCH >= 1 && YK_LAUNCH_SPP >= 1, "launch sizes must be >= 1 sample per pixel");
 #ifndef YK_TILE
 #define YK_TILE 8
@@ -2165,7 +2177,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
   // (A/B knobs: YKGPU_FIRST_LAUNCH, YKGPU_SCHED_GROW — the first launch's samples per pixel and
   // the factor each next launch grows by until kmax)
-  uint32_t first_k = kFirstLaunch, grow_k = 4;
+  uint32_t first_k = kFirstLaunch, grow_k = kSchedGrow;
   if (const char* e = std::getenv("YKGPU_FIRST_LAUNCH")) first_k = (uint32_t)std::max(1, std::atoi(e));
   if (const char* e = std::getenv("YKGPU_SCHED_GROW")) grow_k = (uint32_t)std::max(2, std::atoi(e));
   for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
