@@ -6,9 +6,10 @@ One STEP = one full render of the headline configuration (BASELINE config 3): 19
 the reference's arithmetic.  Inputs (scene, camera) are resident in HBM before the timed region;
 the output RGB8 image is produced in HBM (rank 0 holds the assembled image).
 
-N > 1 (one process per GPU, torchrun): the image's rows are dealt cyclically (row r → rank r mod
-N), each rank renders its tile into device memory, and the tiles are gathered to rank 0 over
-RCCL (torch.distributed 'nccl') and de-interleaved on device — all inside the timed region.
+N > 1 (one process per GPU, torchrun): the image's columns are dealt cyclically in 8-column bands
+(band b → rank b mod N, every row; `--deal rows`: single rows, row r → rank r mod N), each rank
+renders its tile into device memory, and the tiles are gathered to rank 0 over RCCL
+(torch.distributed 'nccl') and de-interleaved on device — all inside the timed region.
 The total image is fixed, so this is STRONG scaling.
 
 Prints ONE JSON line on rank 0.  The `roofline` object is the dominant kernel's VALU roofline
@@ -85,11 +86,12 @@ def pmc_facts(workload=None):
     return {k: rec[k] for k in keep if k in rec}
 
 
-def other_configs(ren, stream, seed0, nthreads, peak_tf):
+def other_configs(ren, stream, seed0, nthreads, peak_tf, deal):
     """BASELINE configs 4 and 5 on this GPU, after the contract line's timed region (rank 0, N=1):
     config 5 = 1920x1080x4096, max_depth 200, the dielectric-heavy glass scene, whole frame (the
     active-ray compaction stress); config 4 = 3840x2160x1024 on the final scene, rank 0's tile of
-    the 8-GPU split (every 8th row from 0: what one GPU renders in the driver's 8-GPU run).  Each:
+    the 8-GPU split under `deal` (tiles.py: every 8th 8-column band, or every 8th row: what one GPU
+    renders in the driver's 8-GPU run).  Each:
     one warm call, one timed call (HIP events around the call on the bench stream), the roofline
     from a counting call, and the timed image's rows compared with the CPU oracle."""
     import numpy as np
@@ -98,21 +100,25 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf):
     import uecraytracing_amd as yk
     from uecraytracing_amd import flops
     from uecraytracing_amd.records import image_height_for, make_params
-    from uecraytracing_amd.tiles import tile_rows
+    from uecraytracing_amd.tiles import rank_tile, tile_image_cols
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
 
     out = {}
     cases = (("config5", "glass", 1920, 4096, 200, None, (17, 1061)),
-             ("config4_rank0_of_8", "final", 3840, 1024, 50, (0, 8), (0, 134)))
+             ("config4_rank0_of_8", "final", 3840, 1024, 50, (0, 8),
+              (0, 134) if deal == "rows" else (0, 1079, 2159)))
     for name, scene, W, spp, depth, split, cmp_rows in cases:
         scene_file = os.path.join(yk.SCENE_DIR, f"{scene}_seed42.yks")
         spheres, cam = yk.read_scene(scene_file)
         ren.set_scene(spheres, cam)
         H = image_height_for(W)
-        rows = tile_rows(split[0], split[1], H) if split else (0, H, 1, 0)
-        tile = torch.empty((rows[1], W, 3), dtype=torch.uint8, device=torch.device("cuda", ren.device))
-        p = make_params(W, H, spp, depth, seed0, rows=rows, flags=0)
+        tk = rank_tile(split[0], split[1], H, W, deal) if split else {"rows": (0, H, 1, 0)}
+        rows = tk["rows"]
+        p = make_params(W, H, spp, depth, seed0, flags=0, **tk)
+        Wt = p.tile_width()
+        xs = (tile_image_cols(split[0], split[1], W) if split and tk.get("cols") else list(range(W)))
+        tile = torch.empty((rows[1], Wt, 3), dtype=torch.uint8, device=torch.device("cuda", ren.device))
         with torch.cuda.stream(stream):
             ren.render_async(p, tile.data_ptr(), stream.cuda_stream)  # warm call (allocations)
             torch.cuda.synchronize()
@@ -124,11 +130,11 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf):
         ms = e0.elapsed_time(e1)
         tst = ren.stats()
         img = tile.cpu().numpy()
-        ren.render_async(make_params(W, H, spp, depth, seed0, rows=rows, flags=1), tile.data_ptr(),
+        ren.render_async(make_params(W, H, spp, depth, seed0, flags=1, **tk), tile.data_ptr(),
                          stream.cuda_stream)
         torch.cuda.synchronize()
         st = ren.stats()
-        n = rows[1] * W * spp
+        n = rows[1] * Wt * spp
         launches = max(1, tst["launches"])
         launch_ms = tst["render_busy_ms"] / launches
         alg = flops.algorithmic(st)
@@ -136,12 +142,15 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf):
         # parity: tile rows cmp_rows (their image rows y) against the oracle at full spp
         ys = [rows[0] + t * rows[2] for t in cmp_rows]
         cpu = np.concatenate([oracle_lib.render(spheres, cam, make_params(W, H, spp, depth, seed0, rows=(y, 1, 1)),
-                                                nthreads=nthreads)[0] for y in ys])
+                                                nthreads=nthreads)[0][:, xs] for y in ys])
         gpu = img[list(cmp_rows)]
         out[name] = {
             "workload": f"{W}x{H}x{spp}spp, max_depth {depth}, {os.path.relpath(scene_file, ROOT)} "
                         f"({len(spheres)} spheres), seed0 {seed0}, mt19937 + FP64"
-                        + (f", rows {rows[0]}::{rows[2]} ({rows[1]} rows = rank {split[0]} of {split[1]})" if split else ""),
+                        + ((f", rows {rows[0]}::{rows[2]} ({rows[1]} rows = rank {split[0]} of {split[1]})"
+                            if deal == "rows" else
+                            f", 8-column bands {split[0]}::{split[1]} ({Wt} columns x {H} rows = rank "
+                            f"{split[0]} of {split[1]})") if split else ""),
             "value": round(n / (ms * 1e-3) / 1e6, 3), "unit": "Msamples/s", "ms": round(ms, 3),
             "samples": n, "launches": launches,
             "roofline": {"bound": "valu", "achieved": round(ach, 4), "peak": peak_tf, "unit": "TFLOP/s",
@@ -157,7 +166,7 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf):
     return out
 
 
-def rank_tiles(ren, stream, seed0, frame_ms):
+def rank_tiles(ren, stream, seed0, frame_ms, deal):
     """The N-GPU bound on this GPU: every rank's row tile of the N-way
     split rendered ALONE (ms per call over 4 back-to-back calls after a warm one, HIP events on the
     bench stream: the per-rank steps of the N-GPU bench), for config 3 at N = 2, 4, 8 and config 4's
@@ -168,7 +177,7 @@ def rank_tiles(ren, stream, seed0, frame_ms):
 
     import uecraytracing_amd as yk
     from uecraytracing_amd.records import image_height_for, make_params
-    from uecraytracing_amd.tiles import tile_rows
+    from uecraytracing_amd.tiles import rank_tile
 
     def call_ms(p, out, calls=4):
         # one warm call, then `calls` back-to-back calls as the N-GPU bench's steps issue them (a
@@ -185,18 +194,22 @@ def rank_tiles(ren, stream, seed0, frame_ms):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / calls
 
-    out = {}
+    out = {"deal": deal}
+    other = "rows" if deal == "cols" else "cols"
     for cfg, W, spp, ns in (("config3", 1920, 512, (2, 4, 8)), ("config4", 3840, 1024, (8,))):
         spheres, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
         ren.set_scene(spheres, cam)
         H = image_height_for(W)
         buf = torch.empty((H, W, 3), dtype=torch.uint8, device=torch.device("cuda", ren.device))
         full = frame_ms if cfg == "config3" else call_ms(make_params(W, H, spp, 50, seed0, flags=0), buf)
-        for n in ns:
-            ms = [call_ms(make_params(W, H, spp, 50, seed0, rows=tile_rows(r, n, H), flags=0), buf) for r in range(n)]
-            out[f"{cfg}_n{n}"] = {"tile_ms": [round(m, 3) for m in ms], "slowest_ms": round(max(ms), 3),
-                                  "frame_ms": round(full, 3), "speedup_bound": round(full / max(ms), 3),
-                                  "slowest_over_ideal": round(max(ms) / (full / n), 4)}
+        # the bench's dealing at every N; the other dealing at N = 8 for comparison
+        for n, d in [(n, deal) for n in ns] + [(8, other)]:
+            ms = [call_ms(make_params(W, H, spp, 50, seed0, flags=0, **rank_tile(r, n, H, W, d)), buf)
+                  for r in range(n)]
+            out[f"{cfg}_n{n}" + ("" if d == deal else f"_{d}")] = {
+                "tile_ms": [round(m, 3) for m in ms], "slowest_ms": round(max(ms), 3),
+                "frame_ms": round(full, 3), "speedup_bound": round(full / max(ms), 3),
+                "slowest_over_ideal": round(max(ms) / (full / n), 4)}
     return out
 
 
@@ -220,6 +233,8 @@ def parse():
                     help="skip the one-call timings of the FP32 and xor128 modes (rank 0, N=1)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the BASELINE config 4 / 5 measurements (rank 0, N=1)")
+    ap.add_argument("--deal", choices=("cols", "rows"), default=None,
+                    help="N-GPU split: 8-column bands over every row (default, tiles.DEAL) or single rows")
     ap.add_argument("--no-tiles", action="store_true",
                     help="skip the per-rank tile timings of the N-GPU splits (rank 0, N=1)")
     return ap.parse_args()
@@ -227,6 +242,9 @@ def parse():
 
 def main():
     args = parse()
+    if args.deal is None:
+        from uecraytracing_amd.tiles import DEAL
+        args.deal = DEAL
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -239,7 +257,7 @@ def main():
     import uecraytracing_amd as yk
     from uecraytracing_amd import flops
     from uecraytracing_amd.records import image_height_for, make_params
-    from uecraytracing_amd.tiles import BAND_LOG2, TileGather, tile_rows
+    from uecraytracing_amd.tiles import BAND_LOG2, COL_BAND_LOG2, TileGather, rank_tile
 
     # one process per GPU; YK_BENCH_BACKEND=gloo (rehearsal only) lets several ranks share a GPU
     backend = os.environ.get("YK_BENCH_BACKEND", "nccl")
@@ -264,9 +282,9 @@ def main():
     else:
         scene_file = None
         spheres, cam = yk.build_scene(args.scene, args.scene_seed)
-    rows = tile_rows(rank, world, H)
-    rows_mine = rows[1]
-    params = make_params(W, H, spp, depth, args.seed0, rows=rows, flags=0)  # production instance
+    tk = rank_tile(rank, world, H, W, args.deal)  # this rank's rows (and columns): tiles.py
+    params = make_params(W, H, spp, depth, args.seed0, flags=0, **tk)  # production instance
+    pix_mine = params.row_count * params.tile_width()
 
     ren = yk.Renderer(local)
     # world + camera uploaded to HBM before any timing (the contract: inputs resident when the
@@ -279,7 +297,7 @@ def main():
         up.append((time.perf_counter() - t) * 1e3)
     scene_upload_ms = sorted(up)[1]
     stream = torch.cuda.Stream(device=dev)
-    tg = TileGather(rank, world, H, W, dev)  # tile, gather buffers and the assembled image
+    tg = TileGather(rank, world, H, W, dev, deal=args.deal)  # tile, gather buffers and the assembled image
     ev = []
 
     def step(timed):
@@ -317,7 +335,7 @@ def main():
     launches = max(1, tst["launches"])
     # work counters: one more launch of the same workload with the counting instance, after the
     # timed region (the work is deterministic, so its counts are the timed launches' counts)
-    ren.render_async(make_params(W, H, spp, depth, args.seed0, rows=rows, flags=1),
+    ren.render_async(make_params(W, H, spp, depth, args.seed0, flags=1, **tk),
                      tg.tile.data_ptr(), stream.cuda_stream)
     torch.cuda.synchronize()
     st = ren.stats()
@@ -338,7 +356,7 @@ def main():
     impl_tf = impl / launches / (launch_ms * 1e-3) / 1e12
     # SURVEY §8(d) algorithmic HBM bytes: the RGB8 image once, the scene once per workgroup
     scene_bytes = len(spheres) * SPHERE_RECORD_BYTES
-    hbm_step = rows_mine * W * 3 + launches * tst["grid_blocks"] * scene_bytes
+    hbm_step = pix_mine * 3 + launches * tst["grid_blocks"] * scene_bytes
     hbm_gbps = hbm_step / launches / (launch_ms * 1e-3) / 1e9
     workload = f"{args.scene}{args.scene_seed}_{W}x{H}x{spp}_d{depth}_n{world}"
     facts = pmc_facts(workload)
@@ -371,7 +389,9 @@ def main():
                         f"seed0 {args.seed0}, mt19937 + FP64 bit-exact",
             "image": f"{W}x{H}", "spp": spp, "max_depth": depth, "spheres": len(spheres),
             "scene_file": os.path.relpath(scene_file, ROOT) if scene_file else None,
-            "partition": f"rows dealt cyclically in bands of {1 << BAND_LOG2} over {world} GPU(s), "
+            "partition": (f"rows dealt cyclically in bands of {1 << BAND_LOG2}" if args.deal == "rows" else
+                          f"columns dealt cyclically in bands of {1 << COL_BAND_LOG2} (every row)")
+                         + f" over {world} GPU(s), "
                          + ("RCCL gather to rank 0" if backend == "nccl" else
                             f"{backend} gather to rank 0 through the host (rehearsal: ranks share a GPU)"),
         },
@@ -411,11 +431,11 @@ def main():
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 7), "traffic": traffic,
                     "traffic_over_algorithmic": round(traffic / (hbm_step / launches), 1) if traffic else None,
                     "device_bytes": tst["device_bytes"], "call_bytes": tst["call_bytes"],
-                    "algorithmic": f"SURVEY §8(d): the RGB8 image ({rows_mine * W * 3} B) once per "
+                    "algorithmic": f"SURVEY §8(d): the RGB8 image ({pix_mine * 3} B) once per "
                                    f"step + the scene ({scene_bytes} B) once per workgroup "
                                    f"({tst['grid_blocks']} per launch); traffic = PMC FETCH_SIZE x2 + "
-                                   f"WRITE_SIZE per launch (scratch: the start records with the colours "
-                                   f"written over them, the processing order, MT fallback state)"},
+                                   f"WRITE_SIZE per launch (scratch: the start records, the colour "
+                                   f"records, the processing order, MT fallback state)"},
             "checks": {"launches_x_launch_ms_le_step": bool(launches * launch_ms <= ms_per_step * 1.001)},
             # render = the launches' spans summed (they overlap); render_busy = their union
             "step_breakdown_ms": {"render_spans_summed": round(tst["kernel_ms"], 3),
@@ -495,7 +515,7 @@ def main():
         scratch = torch.empty_like(tg.tile)
         modes = {}
         for name, kw in (("fp32_mt19937", {"precision": PRECISION_FP32}), ("fp64_xor128", {"rng": RNG_XOR128})):
-            mp = make_params(W, H, spp, depth, args.seed0, rows=tile_rows(rank, world, H), **kw)
+            mp = make_params(W, H, spp, depth, args.seed0, **tk, **kw)
             ren.render_async(mp, scratch.data_ptr(), stream.cuda_stream)  # warm-up call
             torch.cuda.synchronize()
             t = time.perf_counter()
@@ -507,10 +527,11 @@ def main():
         result["modes"] = modes
 
     if rank == 0 and world == 1 and not args.no_configs:
-        result["configs"] = other_configs(ren, stream, args.seed0, args.cpu_threads or usable_cpus()[0], peak_tf)
+        result["configs"] = other_configs(ren, stream, args.seed0, args.cpu_threads or usable_cpus()[0], peak_tf,
+                                          args.deal)
 
     if rank == 0 and world == 1 and not args.no_tiles and (W, spp, depth, args.scene) == (1920, 512, 50, "final"):
-        result["tiles"] = rank_tiles(ren, stream, args.seed0, ms_per_step)
+        result["tiles"] = rank_tiles(ren, stream, args.seed0, ms_per_step, args.deal)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 9u
+#define YKGPU_ABI_VERSION 10u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 (reflected + fuzz * the reference's random_in_unit_sphere,
@@ -141,6 +141,17 @@ typedef struct yk_render_params {
    * row_stride-th band (rank k of N: row_begin = k*B, row_stride = N).  0: single rows.
    * Whole bands keep a wave's pixels adjacent in the image (coherent rays); DESIGN.md §7. */
   uint32_t row_band_log2;
+  /* Column sets (ABI 10; the N-GPU split of uecraytracing_amd/tiles.py): col_count == 0 renders
+   * every column (col_begin, col_stride and col_band_log2 must then be 0).  Otherwise, with
+   * C = 2^col_band_log2, tile column j is image column col_begin + (j / C) * col_stride * C + j % C
+   * — bands of C consecutive columns, every col_stride-th band — and the tile is
+   * row_count x col_count pixels.  Seeds and the camera use the image position (y, x), so any
+   * row and column set renders the image's own pixels.  Bands of 8 columns over every row keep a
+   * rank's 8x8 processing blocks 8x8 in the image (coherent rays). */
+  uint32_t col_begin;
+  uint32_t col_count;
+  uint32_t col_stride;
+  uint32_t col_band_log2;
   uint32_t reserved0;
 } yk_render_params;
 
@@ -204,11 +215,12 @@ int ykgpu_context_destroy(ykgpu_context* ctx);
 int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count,
                     const yk_camera* camera);
 
-/* The render loop (source.cpp:122-172) for the rows named by params, synchronous, into a
- * caller-owned host buffer of row_count * W * 3 bytes laid out like image_t. */
+/* The render loop (source.cpp:122-172) for the rows (and columns) named by params, synchronous,
+ * into a caller-owned host buffer of row_count * Wt * 3 bytes laid out like image_t, where the
+ * tile width Wt is col_count, or W when col_count == 0. */
 int ykgpu_render(ykgpu_context* ctx, const yk_render_params* params, uint8_t* rgb_host);
 
-/* Same, into device memory (row_count * W * 3 bytes on ctx's device), ordered on `stream`
+/* Same, into device memory (row_count * Wt * 3 bytes on ctx's device), ordered on `stream`
  * (a hipStream_t; NULL = the context's own stream): the render starts after the work already
  * queued on `stream` and the image is complete for the work queued after it.  Internally the
  * kernels run on the context's own streams (render launches at the device's top stream
@@ -218,15 +230,15 @@ int ykgpu_render_async(ykgpu_context* ctx, const yk_render_params* params, void*
                        void* stream);
 
 /* Diagnostics: the per-pixel colour sum before to_color3b (source.cpp:137-167), 3 doubles per
- * pixel, row_count * W * 3 doubles, host buffer. */
+ * pixel, row_count * Wt * 3 doubles, host buffer. */
 int ykgpu_render_sums(ykgpu_context* ctx, const yk_render_params* params, double* sums_host);
 
 /* Verbose level 3 (raytracer.hpp:21-25: ray_color prints every ray it is called with, the one
  * reaching depth 0 included).  Renders the rows of params (COUNT_WORK instance) and records, for
- * every sample (index (row_t*W + x)*spp + s over the tile), the first max_rays rays of its path
+ * every sample (index (row_t*Wt + col_t)*spp + s over the tile), the first max_rays rays of its path
  * as 6 doubles each (origin xyz, direction xyz; FP32 rays are floats widened exactly) into
  * rays_host[(index*max_rays + k)*6 ...] and the number of ray_color calls into counts_host[index]
- * (which may exceed max_rays).  row_count * W * spp * max_rays * 48 bytes of device memory are
+ * (which may exceed max_rays).  row_count * Wt * spp * max_rays * 48 bytes of device memory are
  * used for the call, so callers render large images in row bands. */
 int ykgpu_render_trace(ykgpu_context* ctx, const yk_render_params* params, uint32_t max_rays,
                        double* rays_host, uint32_t* counts_host);
@@ -275,7 +287,8 @@ int ykgpu_group_size(const ykgpu_group* group, uint32_t* n);
 int ykgpu_group_set_scene(ykgpu_group* group, const yk_sphere* spheres, uint32_t count,
                           const yk_camera* camera);
 /* The render loop over every entry; synchronous; rgb_host as for ykgpu_render
- * (row_count * W * 3 bytes, the rows of params in order). */
+ * (row_count * tile width * 3 bytes, the rows of params in order).  The entries share the
+ * params' column set; the rows are dealt. */
 int ykgpu_group_render(ykgpu_group* group, const yk_render_params* params, uint8_t* rgb_host);
 /* Statistics of the last group render: index < n the entry's own (its tile), index -1 the whole
  * call: samples and work counters summed over the entries, launches summed, kernel_ms /

@@ -222,18 +222,27 @@ static uint64_t row_y(const yk_render_params* p, uint32_t i) {
   return (uint64_t)p->row_begin + ((((uint64_t)(i >> L)) * p->row_stride) << L) + (i & ((1u << L) - 1u));
 }
 
+/* ... and image column of tile column c of the column set (ABI 10: col_count == 0 = every
+ * column; else bands of 2^col_band_log2 columns, every col_stride-th band) */
+static uint32_t tile_w(const yk_render_params* p) { return p->col_count ? p->col_count : p->image_width; }
+static uint64_t col_x(const yk_render_params* p, uint32_t c) {
+  if (!p->col_count) return c;
+  const uint32_t L = p->col_band_log2;
+  return (uint64_t)p->col_begin + ((((uint64_t)(c >> L)) * p->col_stride) << L) + (c & ((1u << L) - 1u));
+}
+
 static void* worker(void* arg) {
   job_t* j = (job_t*)arg;
   world_t w = {j->s, j->n, j->cam, j->p, 0, j->as_shipped};
-  const uint32_t W = j->p->image_width;
+  const uint32_t Wt = tile_w(j->p);
   /* pixels dealt to the threads one by one (a single row still uses every thread) */
-  const uint64_t npix = (uint64_t)j->p->row_count * W;
+  const uint64_t npix = (uint64_t)j->p->row_count * Wt;
   for (uint64_t k = j->tid; k < npix; k += j->nthreads) {
-    const uint32_t i = (uint32_t)(k / W), x = (uint32_t)(k % W);
-    const uint32_t y = (uint32_t)row_y(j->p, i);
+    const uint32_t i = (uint32_t)(k / Wt), c = (uint32_t)(k % Wt);
+    const uint32_t y = (uint32_t)row_y(j->p, i), x = (uint32_t)col_x(j->p, c);
     {
       c3 ps = pixel_sum(&w, y, x, &j->segs);
-      size_t o = ((size_t)i * W + x) * 3;
+      size_t o = ((size_t)i * Wt + c) * 3;
       if (j->sums) { j->sums[o] = ps.r; j->sums[o + 1] = ps.g; j->sums[o + 2] = ps.b; }
       if (j->rgb) {
         j->rgb[o] = quantise(ps.r, j->p->samples_per_pixel);
@@ -252,6 +261,9 @@ static int check(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_
   if (p->row_count && (p->row_stride == 0 || p->row_band_log2 > 10 ||
       row_y(p, p->row_count - 1) >= p->image_height))
     return YK_ERR_INVALID;
+  if (p->col_count ? (p->col_stride == 0 || p->col_band_log2 > 10 || col_x(p, p->col_count - 1) >= p->image_width)
+                   : (p->col_begin || p->col_stride || p->col_band_log2))
+    return YK_ERR_INVALID;
   if ((p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32) || (p->rng != YK_RNG_MT19937 && p->rng != YK_RNG_XOR128) ||
       p->seed_mode > YK_SEED_RANDOM_DEVICE || (p->seed_mode == YK_SEED_RANDOM_DEVICE && !p->seed_key))
     return YK_ERR_UNSUPPORTED;
@@ -260,8 +272,8 @@ static int check(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_
 
 /* ------------------------------------------------------------------ exported (ctypes) */
 
-/* Render the rows named by p into rgb (row_count*W*3 bytes) and/or sums (row_count*W*3
- * doubles), with `nthreads` host threads over interleaved pixels.  Returns YK_* status;
+/* Render the tile named by p (its rows, and its columns when col_count > 0) into rgb
+ * (row_count*Wt*3 bytes) and/or sums (row_count*Wt*3 doubles), with `nthreads` host threads over interleaved pixels.  Returns YK_* status;
  * *segments / *tests (nullable) receive work counts. */
 static int render_impl(const yk_sphere* s, uint32_t n, const yk_camera* cam, const yk_render_params* p,
                        uint8_t* rgb, double* sums, int nthreads, uint64_t* segments, uint64_t* tests,

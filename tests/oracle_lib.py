@@ -64,7 +64,7 @@ def render(spheres, camera: Camera, params: RenderParams, nthreads=None, want_rg
     """Returns (rgb uint8[rows, W, 3] | None, sums float64[rows, W, 3] | None, segments, tests)."""
     lib = load()
     arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
-    rows, W = params.row_count, params.image_width
+    rows, W = params.row_count, params.tile_width()
     rgb = np.zeros((rows, W, 3), np.uint8) if want_rgb else None
     sums = np.zeros((rows, W, 3), np.float64) if want_sums else None
     segs, tests = ctypes.c_uint64(0), ctypes.c_uint64(0)
@@ -83,7 +83,7 @@ def render_as_shipped(spheres, camera: Camera, params: RenderParams, nthreads=No
     the image is not reproducible.  Returns segments."""
     lib = load()
     arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
-    rgb = np.zeros((params.row_count, params.image_width, 3), np.uint8)
+    rgb = np.zeros((params.row_count, params.tile_width(), 3), np.uint8)
     segs, tests = ctypes.c_uint64(0), ctypes.c_uint64(0)
     nt = nthreads or max(1, min(os.cpu_count() or 1, 8))
     st = lib.yko_render_as_shipped(arr, len(arr), ctypes.byref(camera), ctypes.byref(params),

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = yk.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 9
+    assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 10
 
 
 def test_reference_camera_matches_camera_hpp():
@@ -102,9 +102,21 @@ def test_group_invalid_arguments_are_reported():
     assert lib.ykgpu_group_size(None, ctypes.byref(n)) == 1
 
 
+def test_render_params_layout_matches_the_header():
+    """yk_render_params (include/ykgpu.h, ABI 10): the column set after row_band_log2, 88 bytes."""
+    P = records.RenderParams
+    assert P.t_min.offset == 48 and P.seed_key.offset == 56 and P.row_band_log2.offset == 64
+    assert (P.col_begin.offset, P.col_count.offset, P.col_stride.offset, P.col_band_log2.offset,
+            P.reserved0.offset) == (68, 72, 76, 80, 84)
+    assert ctypes.sizeof(P) == 88
+    p = records.make_params(1920, cols=(8, 240, 8, 3))
+    assert (p.col_begin, p.col_count, p.col_stride, p.col_band_log2) == (8, 240, 8, 3)
+    assert p.tile_width() == 240 and records.make_params(1920).tile_width() == 1920
+
+
 def test_render_stats_layout_matches_the_header():
     """yk_render_stats ends with device_bytes at offset 312, call_bytes at 320 and sclk_mhz at 328
-    (include/ykgpu.h, ABI 9)."""
+    (include/ykgpu.h, ABI 10)."""
     assert records.RenderStats.device_bytes.offset == 312
     assert records.RenderStats.call_bytes.offset == 320
     assert records.RenderStats.sclk_mhz.offset == 328

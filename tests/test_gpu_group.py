@@ -62,6 +62,20 @@ def test_group_final_scene_strided_rows_equal_single(single):
         assert g.stats(-1)["launches"] >= 4
 
 
+def test_group_keeps_the_column_set(single):
+    """A column set (ABI 10) passes through the group: the entries deal its rows and render the
+    same columns; the tile is row_count x col_count."""
+    from uecraytracing_amd.tiles import tile_cols
+    arr, cam = yk.read_scene(f"{yk.SCENE_DIR}/final_seed42.yks")
+    single.set_scene(arr, cam)
+    p = make_params(384, 216, 8, 50, 404, rows=(3, 60, 2), cols=tile_cols(2, 3, 384))
+    want = single.render(p)
+    assert want.shape == (60, 128, 3)
+    with yk.Group([0, 0, 0]) as g:
+        g.set_scene(arr, cam)
+        np.testing.assert_array_equal(g.render(p), want)
+
+
 def test_group_more_entries_than_rows(single):
     """Entries with no row (k > row_count) are skipped."""
     single.set_scene(refscenes.ref4(), refscenes.reference_camera())

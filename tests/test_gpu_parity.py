@@ -206,6 +206,51 @@ def test_banded_rows_of_the_headline_config(ren):
     assert got.tobytes() == want.tobytes()
 
 
+def test_column_tiles_reassemble(ren):
+    """Column sets (ABI 10; bench.py's N-GPU split: 8-column bands over every row), including a
+    partial last band, single columns and a row set with them, in FP64, FP32 and xor128: the tiles
+    reassemble into the reference golden image bit for bit."""
+    from uecraytracing_amd.tiles import tile_cols, tile_image_cols
+    ren.set_scene(refscenes.mixed12(), refscenes.reference_camera())
+    for name, kw in (("mixed12_96x54x16_d50_s404", {}),):
+        e = next(c for c in MAN["cases"] if c["name"] == name)
+        full = golden_data.rgb(e)
+        for n, L in ((2, 3), (3, 3), (8, 3), (5, 0), (7, 2)):
+            out = np.zeros_like(full)
+            for r in range(n):
+                cols = tile_cols(r, n, e["W"], L)
+                if cols[1] == 0:
+                    continue
+                out[:, tile_image_cols(r, n, e["W"], L)] = ren.render(
+                    make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], cols=cols, **kw))
+            np.testing.assert_array_equal(out, full)
+        # a row set and a column set together
+        got = ren.render(make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], rows=(1, 9, 6),
+                                     cols=tile_cols(1, 3, e["W"], 3)))
+        np.testing.assert_array_equal(got, full[1::6][:9][:, tile_image_cols(1, 3, e["W"], 3)])
+    for prec, rng in ((PRECISION_FP32, RNG_MT19937), (PRECISION_FP64, RNG_XOR128)):
+        full = ren.render(make_params(96, 54, 8, 50, 404, precision=prec, rng=rng))
+        for r in range(3):
+            got = ren.render(make_params(96, 54, 8, 50, 404, precision=prec, rng=rng, cols=tile_cols(r, 3, 96)))
+            np.testing.assert_array_equal(got, full[:, tile_image_cols(r, 3, 96)])
+
+
+def test_column_tile_of_the_headline_config(ren):
+    """Rank 3 of 8 at config 3 under bench.py's column dealing (every row, 8-column bands
+    24-31, 88-95, ...): two rows of the tile against the oracle's, sums bit for bit; a column set
+    the image does not hold is rejected."""
+    from uecraytracing_amd.tiles import tile_cols
+    arr, cam = yk.build_scene("final", 42)
+    ren.set_scene(arr, cam)
+    p = make_params(1920, 1080, 32, 50, 404, rows=(700, 2, 1), cols=tile_cols(3, 8, 1920))
+    got = ren.render_sums(p)
+    assert got.shape == (2, 240, 3)
+    _, want, _, _ = oracle_lib.render(arr, cam, p, nthreads=16, want_rgb=False, want_sums=True)
+    assert got.tobytes() == want.tobytes()
+    with pytest.raises(yk.YkError):
+        ren.render(make_params(1920, 1080, 1, 50, 404, cols=(8, 240, 9, 3)))  # last band past 1920
+
+
 def test_repeatable_and_counts(ren):
     arr, cam = yk.build_scene("final", 42)
     ren.set_scene(arr, cam)

@@ -1,5 +1,5 @@
 """Rehearsal of the N-rank render + gather on whatever GPUs the box has (ranks may share one):
-each rank renders its cyclic row tile into device memory through the C-ABI, the tiles go to
+each rank renders its tile (tiles.DEAL: 8-column bands; YK_DEAL=rows: single rows) into device memory through the C-ABI, the tiles go to
 rank 0 through uecraytracing_amd.tiles.TileGather, and rank 0 compares the assembled image with
 a single-process render of the whole image.  Launch with torchrun; YK_BENCH_BACKEND=gloo when
 ranks share a GPU (RCCL needs one GPU per rank).
@@ -16,7 +16,7 @@ import torch.distributed as dist  # noqa: E402
 
 import uecraytracing_amd as yk  # noqa: E402
 from uecraytracing_amd.records import image_height_for, make_params  # noqa: E402
-from uecraytracing_amd.tiles import TileGather, tile_rows  # noqa: E402
+from uecraytracing_amd.tiles import DEAL, TileGather, rank_tile  # noqa: E402
 
 
 def main():
@@ -32,18 +32,19 @@ def main():
     arr, cam = yk.build_scene("final", 42)
     with yk.Renderer(local) as r:
         r.set_scene(arr, cam)
-        rows = tile_rows(rank, world, H)
-        tg = TileGather(rank, world, H, W, dev)
+        deal = os.environ.get("YK_DEAL", DEAL)
+        tg = TileGather(rank, world, H, W, dev, deal=deal)
         s = torch.cuda.Stream(device=dev)
         with torch.cuda.stream(s):
-            r.render_async(make_params(W, H, spp, 50, 404, rows=rows), tg.tile.data_ptr(), s.cuda_stream)
+            r.render_async(make_params(W, H, spp, 50, 404, **rank_tile(rank, world, H, W, deal)),
+                           tg.tile.data_ptr(), s.cuda_stream)
         s.synchronize()
         img = tg.gather()
         torch.cuda.synchronize()
         if rank == 0:
             full = r.render(make_params(W, H, spp, 50, 404))
             same = bool((img.cpu().numpy() == full).all())
-            print(json.dumps({"world": world, "backend": backend, "W": W, "H": H, "spp": spp,
+            print(json.dumps({"world": world, "backend": backend, "deal": deal, "W": W, "H": H, "spp": spp,
                               "identical_to_single_render": same}), flush=True)
             if not same:
                 sys.exit(1)

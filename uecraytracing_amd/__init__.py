@@ -31,7 +31,7 @@ EXPORTS = (
     "ykgpu_group_create", "ykgpu_group_destroy", "ykgpu_group_size", "ykgpu_group_set_scene",
     "ykgpu_group_render", "ykgpu_group_get_stats", "ykgpu_render_devices",
 )
-ABI_VERSION = 9
+ABI_VERSION = 10
 SCENE_DIR = os.path.join(PKG_DIR, "scenes")  # committed scene files of the BASELINE configs
 
 _lib = None
@@ -177,19 +177,19 @@ class Renderer:
 
     def render(self, params: RenderParams) -> np.ndarray:
         """Host RGB8 image of the tile: uint8[row_count, W, 3] (image_t layout)."""
-        out = np.empty((params.row_count, params.image_width, 3), np.uint8)
+        out = np.empty((params.row_count, params.tile_width(), 3), np.uint8)
         _check(self._lib.ykgpu_render(self._ctx, ctypes.byref(params), out.ctypes.data))
         return out
 
     def render_sums(self, params: RenderParams) -> np.ndarray:
-        out = np.empty((params.row_count, params.image_width, 3), np.float64)
+        out = np.empty((params.row_count, params.tile_width(), 3), np.float64)
         _check(self._lib.ykgpu_render_sums(self._ctx, ctypes.byref(params), out.ctypes.data))
         return out
 
     def render_trace(self, params: RenderParams, max_rays: int):
         """ray_color's rays (verbose level 3, raytracer.hpp:21-25) of every sample of the tile:
         (rays float64[row_count, W, spp, max_rays, 6], counts uint32[row_count, W, spp])."""
-        shape = (params.row_count, params.image_width, params.samples_per_pixel)
+        shape = (params.row_count, params.tile_width(), params.samples_per_pixel)
         rays = np.zeros(shape + (max_rays, 6), np.float64)
         counts = np.zeros(shape, np.uint32)
         _check(self._lib.ykgpu_render_trace(self._ctx, ctypes.byref(params), max_rays, rays.ctypes.data,
@@ -278,7 +278,7 @@ class Group:
         _check(self._lib.ykgpu_group_set_scene(self._g, arr, len(arr), ctypes.byref(camera)))
 
     def render(self, params: RenderParams) -> np.ndarray:
-        out = np.empty((params.row_count, params.image_width, 3), np.uint8)
+        out = np.empty((params.row_count, params.tile_width(), 3), np.uint8)
         _check(self._lib.ykgpu_group_render(self._g, ctypes.byref(params), out.ctypes.data))
         return out
 
@@ -293,7 +293,7 @@ def render_devices(devices, spheres, camera: Camera, params: RenderParams) -> np
     lib = load_library()
     arr = spheres if isinstance(spheres, ctypes.Array) else sphere_array(spheres)
     devs = (ctypes.c_int * len(devices))(*devices)
-    out = np.empty((params.row_count, params.image_width, 3), np.uint8)
+    out = np.empty((params.row_count, params.tile_width(), 3), np.uint8)
     _check(lib.ykgpu_render_devices(devs, len(devices), arr, len(arr), ctypes.byref(camera),
                                     ctypes.byref(params), out.ctypes.data))
     return out

@@ -240,7 +240,8 @@ __device__ __forceinline__ void dual_start(const KernelArgs& ka, DPath<Gen>& P, 
   constexpr bool kRandomSeed = (kMode & 2) != 0;
   if (!start) return;
   const uint32_t s = ka.s0 + fdiv(P.slot, ka.nps_m, ka.nps_sh);
-  const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
+  const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh);
+  const uint32_t x = tile_col_x(ka.col_begin, ka.col_stride, ka.col_band, qpix - tr * ka.Wt);
   const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
   const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
   StartRec r;

@@ -114,6 +114,11 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #ifndef YK_SLAB_PAIRS
 #define YK_SLAB_PAIRS 0
 #endif
+// FP32 visit: the slow-axis lower bound taken from the slow axis' own far-plane read (its far
+// bound is void there) instead of a seventh plane read; 0 = the separate read
+#ifndef YK_F32_SLOW_FOLD
+#define YK_F32_SLOW_FOLD 1
+#endif
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
 // Spheres per BVH leaf the kernels' leaf code handles: the FP64 leaf test is loop-free for one
@@ -146,7 +151,7 @@ struct KernelArgs {
   // A launch renders samples [s0, s0 + nsl / npix_slots) of every pixel: sample slot
   // i = s_local * npix_slots + p is sample s0 + s_local of tile pixel order[p].
   uint32_t s0, nsl, npix_slots, seed_mode;  // seed_mode: YK_SEED_*
-  uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
+  uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and the tile width Wt
   uint64_t seed_key;
   const uint32_t* __restrict__ order;  // p → tile pixel (kNoPixel: empty slot of an edge block)
   uint64_t pad_a;                      // (keeps the argument layout the kernels were tuned with)
@@ -174,6 +179,8 @@ struct KernelArgs {
   uint32_t* trace_counts;        //   ray_color calls per sample [q*spp + s]
   uint32_t trace_cap, pad_t;
   unsigned long long* clk;  // this launch's shader-clock probe (YK_CLOCK_*): 4 words
+  // the tile's columns (include/ykgpu.h yk_render_params; the whole width: Wt = W, 0, 1, 0)
+  uint32_t Wt, col_begin, col_stride, col_band;
 };
 
 // Shader-clock probe of a launch: thread 0 of block 0 stores s_memtime (the shader clock) and
@@ -215,6 +222,11 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint32_t m, uint32_t sh) {
 __device__ __forceinline__ uint32_t tile_row_y(uint32_t row_begin, uint32_t row_stride, uint32_t band_log2,
                                                uint32_t t) {
   return row_begin + (((t >> band_log2) * row_stride) << band_log2) + (t & ((1u << band_log2) - 1u));
+}
+// ... and image column of tile column j (bands of 2^col_band columns, every col_stride-th band)
+__device__ __forceinline__ uint32_t tile_col_x(uint32_t col_begin, uint32_t col_stride, uint32_t col_band,
+                                               uint32_t j) {
+  return col_begin + (((j >> col_band) * col_stride) << col_band) + (j & ((1u << col_band) - 1u));
 }
 
 struct Hit {
@@ -379,7 +391,8 @@ constexpr uint32_t kNoStart = 0xffffffffu;
 // 0.5% slower, r03ab).
 struct WarmArgs {
   uint32_t W, spp, seed0, row_begin, row_stride, s0, npix_slots, seed_mode, band_log2;
-  uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and W
+  uint32_t Wt, col_begin, col_stride, col_band;  // the tile's columns (as KernelArgs)
+  uint32_t nps_m, nps_sh, w_m, w_sh;  // fdiv magic numbers of npix_slots and the tile width Wt
   uint32_t lens, H;                   // the camera has a lens (lens_radius > 0); image height
   uint64_t seed_key;
   yk_camera cam;
@@ -401,7 +414,8 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
     const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
     const uint32_t q = wa.order[pp];
     const uint32_t pix = q == kNoPixel ? 0u : q;
-    const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh), xx = pix - tr * wa.W;
+    const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh);
+    const uint32_t xx = tile_col_x(wa.col_begin, wa.col_stride, wa.col_band, pix - tr * wa.Wt);
     const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
     const uint32_t seed = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
     uint32_t x[1] = {seed};
@@ -721,7 +735,8 @@ void yk_render_persistent(KernelArgs ka) {
       // loop only loads them; xor128, and the (never seen) record the warm-up could not
       // complete, start here
       const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
-      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
+      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh);
+      const uint32_t x = tile_col_x(ka.col_begin, ka.col_stride, ka.col_band, qpix - tr * ka.Wt);
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       // seed (uint32 wrap, source.cpp:154-158)
       const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
@@ -1365,7 +1380,8 @@ void yk_render_f32(KernelArgs ka) {
     }
     if (start) {
       const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
-      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh), x = qpix - tr * ka.W;
+      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh);
+      const uint32_t x = tile_col_x(ka.col_begin, ka.col_stride, ka.col_band, qpix - tr * ka.Wt);
       const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
       const uint32_t seed = ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
       bool pre = false;
@@ -1420,8 +1436,62 @@ void yk_render_f32(KernelArgs ka) {
       bool linear = (ka.flags & kFlagLinearScan) || !(a >= 0x1p-60f && a <= 0x1p60f) ||
                     !((double)onorm <= ka.origin_bound);
       if (!linear) {
-        f2 inx, ncx, jfx, fcx, iny, ncy, jfy, fcy, inz, ncz, jfz, fcz;
         const float s = __builtin_sqrtf(a) * ykbvh::kF32Cone;  // the cone's slope (>= kF32Cone |d|)
+        const float tmin_lo = tmin * (1.0f - 0x1p-17f);
+        float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
+#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS
+        // The axes in the order (A, B, C), C the ray's slow axis when it has one (y, then x, then
+        // z, as below; else z).  A slow axis has no far bound, so C's far-plane FMA — the same
+        // quad the slow-axis bound reads — serves as the far bound when the ray has no slow axis
+        // and as the slow-axis lower bound when it has one; two clamps route it (v_med3):
+        //   X = med3(fC, ulo, U') = slow ? U' : min(fC, U')    (ulo = slow ? U' : -inf)
+        //   Y = med3(fC, tmin', H) = slow ? max(fC, tmin') : tmin'   (H = slow ? +inf : tmin')
+        //   tf = min3(fA, fB, X), tn = max(max3(nA, nB, nC), Y)
+        // which are the separate-read test's tf and tn (the same culling decisions, the same
+        // traversal): one 16-byte plane read and two packed FMAs fewer per visit.
+        f2 inA, ncA, jfA, fcA, inB, ncB, jfB, fcB, inC, ncC, jfC, fcC;
+        const char *pA, *pB, *pC;
+        float ulo_sel, hi_sel;  // the ray has a slow axis: (+inf, +inf); else (-inf, tmin')
+        {
+          const float dk[3] = {d.x, d.y, d.z}, ok[3] = {o.x, o.y, o.z};
+          float in[3], nc[3], jf[3], fc[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {  // cone_axis's operands
+            const float sg = dk[k] < 0.0f ? -s : s;
+            in[k] = __builtin_amdgcn_rcpf(dk[k] + sg);
+            nc[k] = -(ok[k] * in[k]);
+            const bool far = fabsf(dk[k]) >= kF32FarAt * s;
+            jf[k] = far ? __builtin_amdgcn_rcpf(dk[k] - sg) * (1.0f + 0x1p-17f) : 0.0f;
+            fc[k] = far ? -(ok[k] * jf[k]) : INFINITY;
+          }
+          const float slow = s * kF32SlowAt;
+          const bool sx = fabsf(d.x) < slow, sy = fabsf(d.y) < slow, sz = fabsf(d.z) < slow;
+          const int kc = sy ? 1 : (sx ? 0 : 2), ka_ = kc == 0 ? 1 : 0, kb_ = kc == 2 ? 1 : 2;
+          // (selects, not indexing: a run-time index would put the arrays in scratch)
+          const auto pick = [](const float* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); };
+          float jc = pick(jf, kc), cc = pick(fc, kc);
+          if (sx || sy || sz) {  // C's far FMA gives the slow-axis bound: (plane - o) / (d - s sign d)
+            const float dc = pick(dk, kc);
+            jc = __builtin_amdgcn_rcpf(dc - (dc < 0.0f ? -s : s));
+            cc = -(pick(ok, kc) * jc);
+          }
+          const float ina = pick(in, ka_), nca = pick(nc, ka_), jfa = pick(jf, ka_), fca = pick(fc, ka_);
+          const float inb = pick(in, kb_), ncb = pick(nc, kb_), jfb = pick(jf, kb_), fcb = pick(fc, kb_);
+          const float inc = pick(in, kc), ncc = pick(nc, kc);
+          inA = f2{ina, ina}, ncA = f2{nca, nca}, jfA = f2{jfa, jfa}, fcA = f2{fca, fca};
+          inB = f2{inb, inb}, ncB = f2{ncb, ncb}, jfB = f2{jfb, jfb}, fcB = f2{fcb, fcb};
+          inC = f2{inc, inc}, ncC = f2{ncc, ncc}, jfC = f2{jc, jc}, fcC = f2{cc, cc};
+          // each axis' (near x4, far x4) plane quads of the ray's direction sign in a WideNode
+          const uint32_t ox = d.x < 0.0f ? 16u : 0u, oy = d.y < 0.0f ? 64u : 48u, oz = d.z < 0.0f ? 112u : 96u;
+          pA = nodes + (ka_ == 0 ? ox : oy);
+          pB = nodes + (kb_ == 1 ? oy : oz);
+          pC = nodes + (kc == 0 ? ox : (kc == 1 ? oy : oz));
+          ulo_sel = (sx || sy || sz) ? INFINITY : -INFINITY;
+          hi_sel = (sx || sy || sz) ? INFINITY : tmin_lo;
+        }
+        float ulo = fminf(ustar_f, ulo_sel);
+#else
+        f2 inx, ncx, jfx, fcx, iny, ncy, jfy, fcy, inz, ncz, jfz, fcz;
         cone_axis(d.x, o.x, s, inx, ncx, jfx, fcx);
         cone_axis(d.y, o.y, s, iny, ncy, jfy, fcy);
         cone_axis(d.z, o.z, s, inz, ncz, jfz, fcz);
@@ -1459,8 +1529,7 @@ void yk_render_f32(KernelArgs ka) {
             }
           }
         }
-        const float tmin_lo = tmin * (1.0f - 0x1p-17f);
-        float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
+#endif
         // U*: proven upper bound of the minimum root (culls with ustar_f = U* (1 + 2^-18)); the
         // candidate list (tuple index, lower bound) as in the FP64 kernel, nc = 5 on overflow
         const float ia = __builtin_amdgcn_rcpf(a);  // a in [2^-60, 2^60] here
@@ -1476,6 +1545,28 @@ void yk_render_f32(KernelArgs ka) {
             if (kCount) ++n_node;
             YK_STAMP_NODE_ITERATION(lane);
             // the FP64 kernel's visit (same planes, margins and visit order), the cone's operands
+#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS
+            const f4 qnA = *(const f4*)(pA + node), qfA = *(const f4*)(pA + node + 16);
+            const f4 qnB = *(const f4*)(pB + node), qfB = *(const f4*)(pB + node + 16);
+            const f4 qnC = *(const f4*)(pC + node), qfC = *(const f4*)(pC + node + 16);
+            const int4 ch = *(const int4*)(nodes + node + 144);
+            bool hk[4];
+            const f2 nA[2] = {__builtin_elementwise_fma(qnA.xy, inA, ncA), __builtin_elementwise_fma(qnA.zw, inA, ncA)};
+            const f2 fA[2] = {__builtin_elementwise_fma(qfA.xy, jfA, fcA), __builtin_elementwise_fma(qfA.zw, jfA, fcA)};
+            const f2 nB[2] = {__builtin_elementwise_fma(qnB.xy, inB, ncB), __builtin_elementwise_fma(qnB.zw, inB, ncB)};
+            const f2 fB[2] = {__builtin_elementwise_fma(qfB.xy, jfB, fcB), __builtin_elementwise_fma(qfB.zw, jfB, fcB)};
+            const f2 nC[2] = {__builtin_elementwise_fma(qnC.xy, inC, ncC), __builtin_elementwise_fma(qnC.zw, inC, ncC)};
+            const f2 fC[2] = {__builtin_elementwise_fma(qfC.xy, jfC, fcC), __builtin_elementwise_fma(qfC.zw, jfC, fcC)};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float c = fC[k >> 1][k & 1];
+              const float x = __builtin_amdgcn_fmed3f(c, ulo, ustar_f);    // C as far bound, or U'
+              const float y = __builtin_amdgcn_fmed3f(c, tmin_lo, hi_sel);  // C as slow bound, or tmin'
+              const float tn = fmaxf(fmaxf(fmaxf(nA[k >> 1][k & 1], nB[k >> 1][k & 1]), nC[k >> 1][k & 1]), y);
+              const float tf = fminf(fminf(fA[k >> 1][k & 1], fB[k >> 1][k & 1]), x);
+              hk[k] = tn <= tf;
+            }
+#else
             const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
             const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
             const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
@@ -1513,6 +1604,7 @@ void yk_render_f32(KernelArgs ka) {
               const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
+#endif
 #endif
             asm volatile("" ::"v"(ch.x), "v"(ch.y), "v"(ch.z), "v"(ch.w));
             if (hk[0] || hk[1] || hk[2] || hk[3]) {
@@ -1564,6 +1656,9 @@ void yk_render_f32(KernelArgs ka) {
               if (ub < ustar) {
                 ustar = ub;
                 ustar_f = ub * (1.0f + 0x1p-18f);
+#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS
+                ulo = fminf(ustar_f, ulo_sel);
+#endif
               }
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
@@ -1919,6 +2014,14 @@ uint64_t host_row_y(const yk_render_params* p, uint32_t t) {
   return (uint64_t)p->row_begin + ((((uint64_t)(t >> L)) * p->row_stride) << L) + (t & ((1u << L) - 1u));
 }
 
+// The tile's width: its column set's size, or the image width (col_count == 0)
+uint32_t tile_width(const yk_render_params* p) { return p->col_count ? p->col_count : p->image_width; }
+uint64_t host_col_x(const yk_render_params* p, uint32_t j) {
+  if (!p->col_count) return j;
+  const uint32_t L = p->col_band_log2;
+  return (uint64_t)p->col_begin + ((((uint64_t)(j >> L)) * p->col_stride) << L) + (j & ((1u << L) - 1u));
+}
+
 // Magic numbers of fdiv (kernel side) for a divisor 1 <= d < 2^31
 void fastdiv(uint32_t d, uint32_t& m, uint32_t& sh) {
   uint32_t l = 0;
@@ -1936,7 +2039,14 @@ int check_params(const ykgpu_context* ctx, const yk_render_params* p) {
   if (!p->row_stride) return fail(YK_ERR_INVALID, "row_stride must be > 0");
   if (p->row_band_log2 > 10) return fail(YK_ERR_INVALID, "row_band_log2 must be <= 10");
   if (host_row_y(p, p->row_count - 1) >= p->image_height) return fail(YK_ERR_INVALID, "row range outside the image");
-  if ((uint64_t)p->row_count * p->image_width >= (1ull << 31))
+  if (p->col_count) {
+    if (!p->col_stride) return fail(YK_ERR_INVALID, "col_stride must be > 0");
+    if (p->col_band_log2 > 10) return fail(YK_ERR_INVALID, "col_band_log2 must be <= 10");
+    if (host_col_x(p, p->col_count - 1) >= p->image_width) return fail(YK_ERR_INVALID, "column range outside the image");
+  } else if (p->col_begin || p->col_stride || p->col_band_log2) {
+    return fail(YK_ERR_INVALID, "col_count == 0 (every column) needs col_begin, col_stride, col_band_log2 == 0");
+  }
+  if ((uint64_t)p->row_count * tile_width(p) >= (1ull << 31))
     return fail(YK_ERR_INVALID, "tile larger than 2^31 pixels");
   if (p->precision != YK_PRECISION_FP64 && p->precision != YK_PRECISION_FP32)
     return fail(YK_ERR_UNSUPPORTED, "precision mode");
@@ -2152,14 +2262,15 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   }
   // image rows per tile row, for the shape of the processing blocks (bands of >= 8 rows: 1,
   // an 8 x 8 block stays inside one band)
-  rc = ensure_order(ctx, p->image_width, p->row_count,
+  rc = ensure_order(ctx, tile_width(p), p->row_count,
                     p->row_count > 1 && p->row_band_log2 < 3 ? p->row_stride : 1);
   if (rc) return rc;
-  // Launch schedule (samples per pixel per launch): 8, then kLaunchSpp (32) per launch, also
-  // capped by the colour budget (32 B per sample slot, kLaunchBytes per launch); the last launch
-  // takes a small remainder with it (1920x1080x512: 8, 15 x 32, 24 = 17 launches).  The first
-  // render waits only for an 8-sample warm-up; every later warm-up is ~0.15x the render before it,
-  // so it finishes underneath.  Each launch ends with the tail of its longest paths (~1 ms), but
+  // Launch schedule (samples per pixel per launch): kFirstLaunch (4), growing by kSchedGrow (2)
+  // up to kmax (kLaunchSpp = 32, or more for a small tile), also capped by the colour budget (32 B
+  // per sample slot, kLaunchBytes per launch); a short remainder is folded into the launches before
+  // it (1920x1080x512: 4, 8, 16, 14 x 32, 18, 18 = 19 launches).  The first render waits only for
+  // a 4-sample warm-up, and each next warm-up, twice the one before, finishes under the render
+  // before it (see kSchedGrow).  Each launch ends with the tail of its longest paths (~1 ms), but
   // launches alternate between two streams, so that drain overlaps the next launch: many
   // mid-sized launches beat a few large ones.  Independent of the image size, which matters
   // for the per-rank tiles of N GPUs.
@@ -2242,6 +2353,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ka.camf.h = (float)p->image_height;
   }
   ka.W = p->image_width;
+  ka.Wt = tile_width(p);
+  ka.col_begin = p->col_count ? p->col_begin : 0;
+  ka.col_stride = p->col_count ? p->col_stride : 1;
+  ka.col_band = p->col_count ? p->col_band_log2 : 0;
   ka.H = p->image_height;
   ka.spp = p->samples_per_pixel;
   ka.max_depth = p->max_depth;
@@ -2288,6 +2403,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     return fail(YK_ERR_INVALID, "YK_FLAG_TRACE_RAYS is set by ykgpu_render_trace only");
   WarmArgs wa;
   wa.W = p->image_width;
+  wa.Wt = ka.Wt;
+  wa.col_begin = ka.col_begin;
+  wa.col_stride = ka.col_stride;
+  wa.col_band = ka.col_band;
   wa.spp = p->samples_per_pixel;
   wa.seed0 = p->seed0;
   wa.row_begin = p->row_begin;
@@ -2304,7 +2423,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.inv_h = ka.inv_h;
   wa.npix_slots = nps;
   fastdiv(nps, wa.nps_m, wa.nps_sh);
-  fastdiv(p->image_width, wa.w_m, wa.w_sh);
+  fastdiv(ka.Wt, wa.w_m, wa.w_sh);
   wa.seed_mode = p->seed_mode;
   wa.seed_key = seed_key;
   wa.order = ctx->d_order;
@@ -2481,7 +2600,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ctx->prev_enqueued = true;
   ctx->dirty = false;
   ctx->stats = yk_render_stats{};
-  ctx->stats.samples = (uint64_t)p->row_count * p->image_width * p->samples_per_pixel;
+  ctx->stats.samples = (uint64_t)p->row_count * tile_width(p) * p->samples_per_pixel;
   ctx->stats.launches = launches;
   ctx->stats.grid_blocks = (uint32_t)grid;
   ctx->stats.seed_key = seed_key;
@@ -2495,7 +2614,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     cb += nlaunch * sizeof(uint32_t) + kCounters * sizeof(unsigned long long);
     if (!x128) cb += 2 * lanes * ykd::kMtN * sizeof(uint32_t);
     cb += 2 * lanes * std::max(1u, p->max_depth > kStackRegs ? p->max_depth : 1u) * sizeof(uint16_t);
-    const uint64_t npix = (uint64_t)p->row_count * p->image_width;
+    const uint64_t npix = (uint64_t)p->row_count * tile_width(p);
     cb += npix * 3 + (sums_dev ? npix * 3 * sizeof(double) : 0);
     ctx->stats.call_bytes = cb;
   }
@@ -2862,7 +2981,7 @@ static int render_host(ykgpu_context* ctx, const yk_render_params* p, uint8_t* r
   if (rc) return rc;
   YK_HIP(hipSetDevice(ctx->device));
   const auto t0 = std::chrono::steady_clock::now();
-  const size_t npix = (size_t)p->row_count * p->image_width;
+  const size_t npix = (size_t)p->row_count * tile_width(p);
   if (npix * 3 > ctx->rgb_cap) {
     (void)hipFree(ctx->d_rgb);
     ctx->d_rgb = nullptr;
@@ -2898,7 +3017,7 @@ int ykgpu_render_trace(ykgpu_context* ctx, const yk_render_params* p, uint32_t m
   int rc = check_params(ctx, p);
   if (rc) return rc;
   if (!max_rays || !rays_host || !counts_host) return fail(YK_ERR_INVALID, "null output or max_rays == 0");
-  const size_t n = (size_t)p->row_count * p->image_width * p->samples_per_pixel;
+  const size_t n = (size_t)p->row_count * tile_width(p) * p->samples_per_pixel;
   YK_HIP(hipSetDevice(ctx->device));
   YK_HIP(hipMalloc(&ctx->d_trace, n * max_rays * 6 * sizeof(double)));
   if (hipMalloc(&ctx->d_trace_counts, n * sizeof(uint32_t)) != hipSuccess) {
@@ -3082,7 +3201,7 @@ int ykgpu_group_render(ykgpu_group* g, const yk_render_params* p, uint8_t* rgb_h
     return fail(YK_ERR_UNSUPPORTED, "a group deals single rows: row_band_log2 must be 0");
   if (k > 1 && (uint64_t)p->row_stride * k >= (1ull << 32)) return fail(YK_ERR_INVALID, "row_stride * devices overflows");
   const auto t0 = std::chrono::steady_clock::now();
-  const size_t row_bytes = (size_t)p->image_width * 3;
+  const size_t row_bytes = (size_t)tile_width(p) * 3;
   std::vector<yk_render_params> sub(k, *p);
   std::vector<uint32_t> rows(k, 0);
   // 1. every entry's tile enqueued on its own device before any copy: the devices run together

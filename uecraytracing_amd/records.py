@@ -85,8 +85,15 @@ class RenderParams(ctypes.Structure):
         ("t_min", ctypes.c_double),
         ("seed_key", ctypes.c_uint64),
         ("row_band_log2", ctypes.c_uint32),  # bands of 2^k rows (include/ykgpu.h)
+        ("col_begin", ctypes.c_uint32),  # column set (ABI 10); col_count == 0: every column
+        ("col_count", ctypes.c_uint32),
+        ("col_stride", ctypes.c_uint32),
+        ("col_band_log2", ctypes.c_uint32),
         ("reserved0", ctypes.c_uint32),
     ]
+
+    def tile_width(self) -> int:
+        return self.col_count or self.image_width
 
 
 class RenderStats(ctypes.Structure):
@@ -128,7 +135,7 @@ class RenderStats(ctypes.Structure):
 
 assert ctypes.sizeof(Sphere) == 80
 assert ctypes.sizeof(Camera) == 19 * 8
-assert ctypes.sizeof(RenderParams) == 72
+assert ctypes.sizeof(RenderParams) == 88
 assert ctypes.sizeof(RenderStats) == 336
 
 
@@ -139,13 +146,15 @@ def image_height_for(width: int) -> int:
 
 def make_params(width, height=None, spp=8, max_depth=50, seed0=SEED0_EPOCH0, rows=None,
                 flags=0, t_min=T_MIN, precision=PRECISION_FP64, seed_mode=SEED_COUNTER,
-                seed_key=0, rng=RNG_MT19937) -> RenderParams:
-    """rows = (row_begin, row_count, row_stride[, row_band_log2]); default: the whole image."""
+                seed_key=0, rng=RNG_MT19937, cols=None) -> RenderParams:
+    """rows = (row_begin, row_count, row_stride[, row_band_log2]); default: the whole image.
+    cols = (col_begin, col_count, col_stride[, col_band_log2]); default: every column."""
     if height is None:
         height = image_height_for(width)
     rb, rc, rs, band = (tuple(rows) + (0,))[:4] if rows is not None else (0, height, 1, 0)
+    cb, cc, cs, cband = (tuple(cols) + (0,))[:4] if cols is not None else (0, 0, 0, 0)
     return RenderParams(width, height, spp, max_depth, seed0 & 0xFFFFFFFF, rb, rc, rs,
-                        precision, rng, flags, seed_mode, t_min, seed_key, band, 0)
+                        precision, rng, flags, seed_mode, t_min, seed_key, band, cb, cc, cs, cband, 0)
 
 
 def sphere_array(spheres) -> ctypes.Array:

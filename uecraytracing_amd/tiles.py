@@ -1,4 +1,4 @@
-"""Row tiling of one image across ranks (one process per GPU) and the gather to rank 0.
+"""Tiling of one image across ranks (one process per GPU) and the gather to rank 0.
 
 Every sample's random stream depends only on (y, x, s) (source.cpp:154-158) and every pixel is
 independent, so any partition of the rows renders byte-identical pixels.  Rows are dealt in
@@ -12,10 +12,20 @@ contiguous uint8[rows_max, W, 3] buffer in HBM (padded to the largest tile so th
 moves equal-sized buffers), the tiles are gathered to rank 0 with one collective (RCCL over xGMI
 with backend 'nccl'; 'gloo' on CPU tensors in the tests), and rank 0 de-interleaves them with one
 index_select.
+
+Column dealing (round 4, the default of the N-rank bench: DEAL = "cols"): every rank renders
+every row, and the columns are dealt in bands of 2^COL_BAND_LOG2 = 8, band b → rank b mod N.
+A rank's 8x8 processing blocks are then 8x8 blocks of the IMAGE, as in the single-GPU frame,
+where a row-dealt tile's blocks span 8 x 16 to 32 x 16 image pixels (every N-th row) and their
+rays diverge more.  Columns vary in cost far less than rows (the sky is at the
+top), so cyclic 8-column bands balance the ranks as well.  The tile is uint8[H, cols_max, 3];
+rank 0 de-interleaves the gathered tiles with one index_select over pixels.
 """
 from __future__ import annotations
 
 BAND_LOG2 = 0
+COL_BAND_LOG2 = 3
+DEAL = "cols"
 
 
 def tile_rows(rank: int, world: int, height: int, band_log2: int = BAND_LOG2):
@@ -48,19 +58,68 @@ def assembly_index(world: int, height: int, device=None, band_log2: int = BAND_L
     return torch.tensor(idx, device=device)
 
 
+def tile_cols(rank: int, world: int, width: int, band_log2: int = COL_BAND_LOG2):
+    """(col_begin, col_count, col_stride, col_band_log2) of rank's column set — the C-ABI's
+    column set (include/ykgpu.h yk_render_params, ABI 10)."""
+    return tile_rows(rank, world, width, band_log2)
+
+
+def tile_image_cols(rank: int, world: int, width: int, band_log2: int = COL_BAND_LOG2):
+    """Image column of each of rank's tile columns, in tile order."""
+    return tile_image_rows(rank, world, width, band_log2)
+
+
+def rank_tile(rank: int, world: int, height: int, width: int, deal: str = DEAL) -> dict:
+    """make_params keyword arguments (rows=, cols=) of rank's tile under `deal` ("rows" or
+    "cols")."""
+    if deal == "rows":
+        return {"rows": tile_rows(rank, world, height)}
+    if deal == "cols":
+        return {"rows": (0, height, 1, 0),
+                "cols": tile_cols(rank, world, width) if world > 1 else None}
+    raise ValueError(f"deal must be 'rows' or 'cols', not {deal!r}")
+
+
+def pixel_assembly_index(world: int, height: int, width: int, device=None,
+                         band_log2: int = COL_BAND_LOG2):
+    """Column dealing: image pixel (y, x) is pixel (y, j) of rank (x // C) % world's padded tile
+    (height x cols_max), the tiles stacked rank after rank; flattened pixel indices."""
+    import torch
+    cm = rows_max(world, width, band_log2)
+    col_src = [0] * width
+    for r in range(world):
+        for j, x in enumerate(tile_image_cols(r, world, width, band_log2)):
+            col_src[x] = (r, j)
+    rank_of = torch.tensor([c[0] for c in col_src], dtype=torch.int64)
+    j_of = torch.tensor([c[1] for c in col_src], dtype=torch.int64)
+    y = torch.arange(height, dtype=torch.int64)[:, None]
+    idx = (rank_of[None, :] * height + y) * cm + j_of[None, :]
+    return idx.reshape(-1).to(device)
+
+
 class TileGather:
     """Gather of the per-rank tiles into the whole image on rank 0 (pre-allocated buffers, so
     the timed loop allocates nothing)."""
 
-    def __init__(self, rank: int, world: int, height: int, width: int, device, band_log2: int = BAND_LOG2):
+    def __init__(self, rank: int, world: int, height: int, width: int, device, band_log2: int | None = None,
+                 deal: str = "rows"):
         import torch
+        if deal not in ("rows", "cols"):
+            raise ValueError(f"deal must be 'rows' or 'cols', not {deal!r}")
+        if band_log2 is None:
+            band_log2 = COL_BAND_LOG2 if deal == "cols" else BAND_LOG2
         self.rank, self.world, self.height, self.width = rank, world, height, width
-        self.rm = rows_max(world, height, band_log2)
-        self.tile = torch.zeros((self.rm, width, 3), dtype=torch.uint8, device=device)
+        self.deal = deal if world > 1 else "rows"
+        if self.deal == "cols":  # tile: every row, cols_max columns (band_log2: the column bands)
+            self.rm, self.cm = height, rows_max(world, width, band_log2)
+        else:
+            self.rm, self.cm = rows_max(world, height, band_log2), width
+        self.tile = torch.zeros((self.rm, self.cm, 3), dtype=torch.uint8, device=device)
         self.image = torch.empty((height, width, 3), dtype=torch.uint8, device=device)
-        self.gathered = (torch.empty((world, self.rm, width, 3), dtype=torch.uint8, device=device)
+        self.gathered = (torch.empty((world, self.rm, self.cm, 3), dtype=torch.uint8, device=device)
                          if rank == 0 and world > 1 else None)
-        self.index = assembly_index(world, height, device, band_log2)
+        self.index = (pixel_assembly_index(world, height, width, device, band_log2) if self.deal == "cols"
+                      else assembly_index(world, height, device, band_log2))
 
     def gather(self):
         """Collective + de-interleave; after it, rank 0's self.image holds the whole image."""
@@ -79,6 +138,10 @@ class TileGather:
         else:
             dist.gather(self.tile, list(self.gathered.unbind(0)) if self.rank == 0 else None, dst=0)
         if self.rank == 0:
-            torch.index_select(self.gathered.reshape(self.world * self.rm, self.width, 3), 0,
-                               self.index, out=self.image)
+            if self.deal == "cols":
+                torch.index_select(self.gathered.reshape(-1, 3), 0, self.index,
+                                   out=self.image.view(self.height * self.width, 3))
+            else:
+                torch.index_select(self.gathered.reshape(self.world * self.rm, self.width, 3), 0,
+                                   self.index, out=self.image)
         return self.image
