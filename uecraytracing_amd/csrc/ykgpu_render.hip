@@ -108,16 +108,24 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #define YK_RENDER_PRIO 1
 #endif
 // the visit's slab constants as one op_sel-read register pair per axis and bound (yk_slab.hpp):
-// 123 -> 115 VGPRs (FP64), 125 -> 111 (FP32), but no faster (512 spp: FP64 173.9 -> 174.1 ms,
-// FP32 194.2 -> 195.2 ms, profiles/r04_ab/); the one-path kernels keep the broadcast pairs,
-// yk_render_dual (which needs the registers) uses them always
-#ifndef YK_SLAB_PAIRS
-#define YK_SLAB_PAIRS 0
+// FP64 123 -> 115 VGPRs and no faster (512 spp 173.9 -> 174.2 ms: the FP64 kernel keeps the
+// broadcast pairs); FP32 125 -> 111 VGPRs and faster (195.3 -> 190.1 ms, profiles/r04_ab/f32/);
+// yk_render_dual (which needs the registers) uses them always.  YK_SLAB_PAIRS sets both (A/B).
+#ifdef YK_SLAB_PAIRS
+#define YK_SLAB_PAIRS_F64 YK_SLAB_PAIRS
+#define YK_SLAB_PAIRS_F32 YK_SLAB_PAIRS
+#endif
+#ifndef YK_SLAB_PAIRS_F64
+#define YK_SLAB_PAIRS_F64 0
+#endif
+#ifndef YK_SLAB_PAIRS_F32
+#define YK_SLAB_PAIRS_F32 1
 #endif
 // FP32 visit: the slow-axis lower bound taken from the slow axis' own far-plane read (its far
-// bound is void there) instead of a seventh plane read; 0 = the separate read
+// bound is void there) instead of a seventh plane read: one read and two packed
+// FMAs fewer per visit, but slower (512 spp 195.3 -> 199.0 ms, profiles/r04_ab/f32/): off
 #ifndef YK_F32_SLOW_FOLD
-#define YK_F32_SLOW_FOLD 1
+#define YK_F32_SLOW_FOLD 0
 #endif
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
@@ -834,7 +842,7 @@ void yk_render_persistent(KernelArgs ka) {
         // relative error inside the 2^-17 margin
         const float ixs = ix * kFar, iys = iy * kFar, izs = iz * kFar;
         const float ox_f = (float)o.x, oy_f = (float)o.y, oz_f = (float)o.z;
-#if YK_SLAB_PAIRS
+#if YK_SLAB_PAIRS_F64
         // per axis ONE register pair (1/d, -o/d) (near) and (c/d, -o c/d) (far), read by op_sel
         // (yk_slab.hpp): 12 VGPRs instead of 24
         const f2 sxp = {ix, -oix}, syp = {iy, -oiy}, szp = {iz, -oiz};
@@ -873,7 +881,7 @@ void yk_render_persistent(KernelArgs ka) {
             const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
             const int4 ch = *(const int4*)(nodes + node + 144);
             bool hk[4];
-#if YK_SLAB_PAIRS
+#if YK_SLAB_PAIRS_F64
             const f2 nx[2] = {slab_fma(qnx.xy, sxp), slab_fma(qnx.zw, sxp)};
             const f2 fx[2] = {slab_fma(qfx.xy, fxp), slab_fma(qfx.zw, fxp)};
             const f2 ny[2] = {slab_fma(qny.xy, syp), slab_fma(qny.zw, syp)};
@@ -1285,7 +1293,7 @@ __device__ __forceinline__ void cone_axis(float dk, float ok, float s, f2& in2, 
   const bool far = fabsf(dk) >= kF32FarAt * s;
   const float jf = far ? __builtin_amdgcn_rcpf(dk - sg) * (1.0f + 0x1p-17f) : 0.0f;
   const float nc = -(ok * in), fc = far ? -(ok * jf) : INFINITY;
-#if YK_SLAB_PAIRS
+#if YK_SLAB_PAIRS_F32
   // the pairs (in, nc) and (jf, fc), read by op_sel (yk_slab.hpp); nc2 / fc2 unused
   in2 = f2{in, nc};
   jf2 = f2{jf, fc};
@@ -1439,7 +1447,7 @@ void yk_render_f32(KernelArgs ka) {
         const float s = __builtin_sqrtf(a) * ykbvh::kF32Cone;  // the cone's slope (>= kF32Cone |d|)
         const float tmin_lo = tmin * (1.0f - 0x1p-17f);
         float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
-#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS
+#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS_F32
         // The axes in the order (A, B, C), C the ray's slow axis when it has one (y, then x, then
         // z, as below; else z).  A slow axis has no far bound, so C's far-plane FMA — the same
         // quad the slow-axis bound reads — serves as the far bound when the ray has no slow axis
@@ -1505,7 +1513,7 @@ void yk_render_f32(KernelArgs ka) {
         // bound like a near distance (same FMA form and error).  Without it, a
         // ray grazing a field of boxes enters every box under its path.  One slow axis per ray
         // gets the bound (y, then x, then z); the others keep L = -inf.
-#if YK_SLAB_PAIRS
+#if YK_SLAB_PAIRS_F32
         f2 jl2 = {0.0f, -INFINITY};  // the (jl, cl) pair
 #else
         f2 jl2 = {0.0f, 0.0f}, cl2 = {-INFINITY, -INFINITY};
@@ -1519,7 +1527,7 @@ void yk_render_f32(KernelArgs ka) {
           for (int k = 0; k < 3; ++k) {
             if (fabsf(dk[k]) < slow) {
               const float jl = __builtin_amdgcn_rcpf(dk[k] - (dk[k] < 0.0f ? -s : s));
-#if YK_SLAB_PAIRS
+#if YK_SLAB_PAIRS_F32
               jl2 = f2{jl, -(ok[k] * jl)};  // (jl, cl), read by op_sel
 #else
               jl2 = f2{jl, jl};
@@ -1545,7 +1553,7 @@ void yk_render_f32(KernelArgs ka) {
             if (kCount) ++n_node;
             YK_STAMP_NODE_ITERATION(lane);
             // the FP64 kernel's visit (same planes, margins and visit order), the cone's operands
-#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS
+#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS_F32
             const f4 qnA = *(const f4*)(pA + node), qfA = *(const f4*)(pA + node + 16);
             const f4 qnB = *(const f4*)(pB + node), qfB = *(const f4*)(pB + node + 16);
             const f4 qnC = *(const f4*)(pC + node), qfC = *(const f4*)(pC + node + 16);
@@ -1573,7 +1581,7 @@ void yk_render_f32(KernelArgs ka) {
             const int4 ch = *(const int4*)(nodes + node + 144);
             const f4 qsl = *(const f4*)(pl + node);
             bool hk[4];
-#if YK_SLAB_PAIRS
+#if YK_SLAB_PAIRS_F32
             const f2 nx[2] = {slab_fma(qnx.xy, inx), slab_fma(qnx.zw, inx)};
             const f2 fx[2] = {slab_fma(qfx.xy, jfx), slab_fma(qfx.zw, jfx)};
             const f2 ny[2] = {slab_fma(qny.xy, iny), slab_fma(qny.zw, iny)};
@@ -1656,7 +1664,7 @@ void yk_render_f32(KernelArgs ka) {
               if (ub < ustar) {
                 ustar = ub;
                 ustar_f = ub * (1.0f + 0x1p-18f);
-#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS
+#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS_F32
                 ulo = fminf(ustar_f, ulo_sel);
 #endif
               }
@@ -2142,6 +2150,14 @@ constexpr uint32_t kFirstLaunch = YK_FIRST_LAUNCH;  // samples per pixel in the 
 #define YK_SCHED_GROW 2
 #endif
 constexpr uint32_t kSchedGrow = YK_SCHED_GROW;
+// ... and for a call enqueued while the previous one still runs (launch(): `inflight`)
+#ifndef YK_FIRST_LAUNCH_OV
+#define YK_FIRST_LAUNCH_OV 32
+#endif
+#ifndef YK_SCHED_GROW_OV
+#define YK_SCHED_GROW_OV 4
+#endif
+constexpr uint32_t kFirstLaunchOv = YK_FIRST_LAUNCH_OV, kSchedGrowOv = YK_SCHED_GROW_OV;
 static_assert(YK_FIRST_LAUNCH >= 1 && YK_LAUNCH_SPP >= 1, "launch sizes must be >= 1 sample per pixel");
 #ifndef YK_TILE
 #define YK_TILE 8
@@ -2198,9 +2214,12 @@ hipError_t create_render_stream(hipStream_t* s) {
 }
 
 // Colour buffers in flight (YKGPU_COL_RING overrides): render c writes buffer c % ring and waits
-// for the reduce of launch c - ring
+// for the reduce of launch c - ring.  Two suffice: a reduce (~0.6 ms for 32 spp of 1920x1080)
+// ends long before the render after next needs its buffer; rings of 2 / 3 / 4 time the same
+// (bench 171.8 / 171.8 / 172.1 ms; config-4 rank tile 174.0 vs 173.6 ms, profiles/r04_ab/rings/)
+// and 2 holds 4.2 GB less at the headline size (call_bytes 22.3 -> 18.1 GB)
 #ifndef YK_COL_RING
-#define YK_COL_RING 4
+#define YK_COL_RING 2
 #endif
 uint32_t col_ring() {
   uint32_t r = YK_COL_RING;
@@ -2281,16 +2300,30 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // a thin row tile at high spp would otherwise run dozens of launches that each pay a ramp and
   // a drain.  Neither floor nor cap exceeds the colour budget or 2^31 slots.
   const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
-  const uint64_t slot_spp = (kLaunchSlots + nps - 1) / nps;
+  uint64_t launch_slots = kLaunchSlots;  // (A/B knob: YKGPU_LAUNCH_SLOTS)
+  if (const char* e = std::getenv("YKGPU_LAUNCH_SLOTS")) launch_slots = (uint64_t)std::max(1ll, std::atoll(e));
+  const uint64_t slot_spp = (launch_slots + nps - 1) / nps;
+  uint64_t launch_spp = kLaunchSpp;  // (A/B knob: YKGPU_LAUNCH_SPP)
+  if (const char* e = std::getenv("YKGPU_LAUNCH_SPP")) launch_spp = (uint64_t)std::max(1, std::atoi(e));
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
-                             std::max<uint64_t>({kLaunchSpp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
+                             std::max<uint64_t>({launch_spp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
-  // (A/B knobs: YKGPU_FIRST_LAUNCH, YKGPU_SCHED_GROW — the first launch's samples per pixel and
-  // the factor each next launch grows by until kmax)
-  uint32_t first_k = kFirstLaunch, grow_k = kSchedGrow;
-  if (const char* e = std::getenv("YKGPU_FIRST_LAUNCH")) first_k = (uint32_t)std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("YKGPU_SCHED_GROW")) grow_k = (uint32_t)std::max(2, std::atoi(e));
+  // A call enqueued while the previous one still runs (back-to-back steps) starts its first
+  // warm-ups under the previous call's last launches, so it needs no small first launch:
+  // kFirstLaunchOv (32), growing by kSchedGrowOv (4) up to kmax: the frame is 16 launches of 32
+  // (bench 8 steps: 172.4 ms per step with 4, 8, 16, 32; 170.8 with 8, 32; 168.4 with 32, 32, ...;
+  // profiles/r04_ab/schedule/)
+  // (A/B knobs: YKGPU_FIRST_LAUNCH, YKGPU_SCHED_GROW and their _OV forms — the first launch's
+  // samples per pixel and the factor each next launch grows by until kmax)
+  bool inflight = false;
+  if (ctx->prev_enqueued && !ctx->dirty && ctx->prev_n > 0 && ctx->lev.size() >= 6ull * ctx->prev_n)
+    inflight = hipEventQuery(ctx->lev[6 * (ctx->prev_n - 1) + 5]) == hipErrorNotReady;
+  uint32_t first_k = inflight ? kFirstLaunchOv : kFirstLaunch, grow_k = inflight ? kSchedGrowOv : kSchedGrow;
+  if (const char* e = std::getenv(inflight ? "YKGPU_FIRST_LAUNCH_OV" : "YKGPU_FIRST_LAUNCH"))
+    first_k = (uint32_t)std::max(1, std::atoi(e));
+  if (const char* e = std::getenv(inflight ? "YKGPU_SCHED_GROW_OV" : "YKGPU_SCHED_GROW"))
+    grow_k = (uint32_t)std::max(2, std::atoi(e));
   for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
     uint32_t take = std::min(k, spp - s0);
     const uint32_t rest = spp - (s0 + take);
