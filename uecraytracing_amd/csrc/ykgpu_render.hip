@@ -1976,7 +1976,8 @@ struct ykgpu_context {
   // stream across calls
   std::vector<hipEvent_t> lev_prev;
   uint32_t prev_n = 0, prev_R = 0, prev_CR = 0;
-  uint64_t prev_geom = 0;  // hash of (slots per launch buffer, record size, ring buffers)
+  uint64_t prev_geom = 0;   // hash of (slots per launch buffer, record size, ring buffers)
+  uint64_t prev_shape = 0;  // (nps, kmax, precision, engine) of the previous call: launch() `inflight`
   bool prev_ok = false;
   bool prev_enqueued = false;  // the previous call's launches were all enqueued (its events exist)
   bool dirty = false;          // a call failed part-way: its enqueued work is not tracked
@@ -2150,9 +2151,11 @@ constexpr uint32_t kFirstLaunch = YK_FIRST_LAUNCH;  // samples per pixel in the 
 #define YK_SCHED_GROW 2
 #endif
 constexpr uint32_t kSchedGrow = YK_SCHED_GROW;
-// ... and for a call enqueued while the previous one still runs (launch(): `inflight`)
+// ... and for a call enqueued while the previous one still runs (launch(): `inflight`): every
+// launch at kmax (YK_FIRST_LAUNCH_OV 0; else that many samples per pixel first, growing by
+// YK_SCHED_GROW_OV)
 #ifndef YK_FIRST_LAUNCH_OV
-#define YK_FIRST_LAUNCH_OV 32
+#define YK_FIRST_LAUNCH_OV 0
 #endif
 #ifndef YK_SCHED_GROW_OV
 #define YK_SCHED_GROW_OV 4
@@ -2310,16 +2313,21 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
                              std::max<uint64_t>({launch_spp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
   std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
   // A call enqueued while the previous one still runs (back-to-back steps) starts its first
-  // warm-ups under the previous call's last launches, so it needs no small first launch:
-  // kFirstLaunchOv (32), growing by kSchedGrowOv (4) up to kmax: the frame is 16 launches of 32
-  // (bench 8 steps: 172.4 ms per step with 4, 8, 16, 32; 170.8 with 8, 32; 168.4 with 32, 32, ...;
-  // profiles/r04_ab/schedule/)
+  // warm-ups under the previous call's last launches, so it needs no small first launch: every
+  // launch at kmax — the frame is 16 launches of 32 (bench 8 steps: 172.4 ms per step with 4, 8,
+  // 16, 32; 170.8 with 8, 32; 168.4 with 32, 32, ...; profiles/r04_ab/schedule/), the 8-way tile
+  // of config 3 four of ~130 (23.1 ms per call starting at 32, 21.8 at 128; the 4-way tile 44.3
+  // -> 43.0 ms starting at 64; profiles/r04_ab/tiles/)
   // (A/B knobs: YKGPU_FIRST_LAUNCH, YKGPU_SCHED_GROW and their _OV forms — the first launch's
   // samples per pixel and the factor each next launch grows by until kmax)
+  // (only for a call of the previous one's shape, whose rings it can overlap: launch() `ov`)
+  const uint64_t shape = ((uint64_t)nps << 24) ^ ((uint64_t)kmax << 2) ^ (f32 ? 2u : 0u) ^ (x128 ? 1u : 0u);
   bool inflight = false;
-  if (ctx->prev_enqueued && !ctx->dirty && ctx->prev_n > 0 && ctx->lev.size() >= 6ull * ctx->prev_n)
+  if (ctx->prev_enqueued && ctx->prev_ok && !ctx->dirty && ctx->prev_shape == shape && ctx->prev_n > 0 &&
+      ctx->lev.size() >= 6ull * ctx->prev_n)
     inflight = hipEventQuery(ctx->lev[6 * (ctx->prev_n - 1) + 5]) == hipErrorNotReady;
-  uint32_t first_k = inflight ? kFirstLaunchOv : kFirstLaunch, grow_k = inflight ? kSchedGrowOv : kSchedGrow;
+  uint32_t first_k = inflight ? (kFirstLaunchOv ? kFirstLaunchOv : kmax) : kFirstLaunch;
+  uint32_t grow_k = inflight ? kSchedGrowOv : kSchedGrow;
   if (const char* e = std::getenv(inflight ? "YKGPU_FIRST_LAUNCH_OV" : "YKGPU_FIRST_LAUNCH"))
     first_k = (uint32_t)std::max(1, std::atoi(e));
   if (const char* e = std::getenv(inflight ? "YKGPU_SCHED_GROW_OV" : "YKGPU_SCHED_GROW"))
@@ -2629,6 +2637,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ctx->prev_R = kWarmRing;
   ctx->prev_CR = kColRing;
   ctx->prev_geom = geom;
+  ctx->prev_shape = shape;
   ctx->prev_ok = !x128 && !warm_first;
   ctx->prev_enqueued = true;
   ctx->dirty = false;
