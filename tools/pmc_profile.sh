@@ -4,7 +4,7 @@
 # PMC_GROUPS (optional): counter groups separated by ';' (default: the roofline set below).
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:---steps 1 --warmup 1 --no-cpu-baseline --no-modes --no-configs}
+ARGS=${@:---steps 1 --warmup 1 --no-cpu-baseline --no-modes --no-configs --no-tiles}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
 mkdir -p $R/$OUT
