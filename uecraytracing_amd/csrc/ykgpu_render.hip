@@ -1961,7 +1961,7 @@ struct ykgpu_context {
   double* d_acc = nullptr;     // running per-pixel sums between launches
   size_t col_cap = 0, acc_cap = 0;
   uint32_t* d_order = nullptr;  // processing slot → tile pixel, for (order_w, order_rows)
-  uint32_t order_w = 0, order_rows = 0, order_slots = 0, order_stride = 0;
+  uint32_t order_w = 0, order_rows = 0, order_slots = 0, order_stride = 0, order_mode = 0;
   size_t warm_cap = 0;
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;  // the MT warm-ups run here, beside the render launches
@@ -2175,7 +2175,12 @@ constexpr uint32_t kTile = YK_TILE;  // processing blocks of kTile x kTile pixel
 // wave starts together stay coherent (8 x 8 tile blocks of a 4-way tile, 8 x 32 image pixels,
 // cost 17% more per sample, measured).
 int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride) {
-  if (ctx->d_order && ctx->order_w == W && ctx->order_rows == rows && ctx->order_stride == stride) return YK_OK;
+  // (A/B knob: YKGPU_ORDER=1 takes the block rows bottom-up)
+  const char* oe = std::getenv("YKGPU_ORDER");
+  const uint32_t mode = oe ? (uint32_t)std::atoi(oe) : 0u;
+  if (ctx->d_order && ctx->order_w == W && ctx->order_rows == rows && ctx->order_stride == stride &&
+      ctx->order_mode == mode)
+    return YK_OK;
   std::vector<uint32_t> ord;
   if (kTile == 0) {
     ord.resize((size_t)W * rows);
@@ -2185,9 +2190,10 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride)
     const uint32_t tw = kTile * kTile / th;
     const uint32_t bx = (W + tw - 1) / tw, by = (rows + th - 1) / th;
     ord.reserve((size_t)bx * by * tw * th);
-    for (uint32_t j = 0; j < by; ++j)
+    for (uint32_t jj = 0; jj < by; ++jj)
       for (uint32_t i = 0; i < bx; ++i)
         for (uint32_t k = 0; k < tw * th; ++k) {
+          const uint32_t j = mode == 1 ? by - 1 - jj : jj;
           const uint32_t x = i * tw + k % tw, y = j * th + k / tw;
           ord.push_back(x < W && y < rows ? y * W + x : kNoPixel);
         }
@@ -2201,6 +2207,7 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride)
   ctx->order_w = W;
   ctx->order_rows = rows;
   ctx->order_stride = stride;
+  ctx->order_mode = mode;
   ctx->order_slots = (uint32_t)ord.size();
   return YK_OK;
 }
