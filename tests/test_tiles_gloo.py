@@ -39,7 +39,8 @@ def _worker(rank, world, port, W, H, spp, out_path, band_log2, deal):
     rgb, _, _, _ = oracle_lib.render(refscenes.mixed12(), refscenes.reference_camera(),
                                      make_params(W, H, spp, 50, 404, **kw), nthreads=2)
     tg = TileGather(rank, world, H, W, "cpu", band_log2, deal=deal)
-    tg.tile[: rgb.shape[0], : rgb.shape[1]] = torch.from_numpy(rgb)
+    # as the C-ABI writes it: the tile's rows x its own width, contiguous from the buffer's start
+    tg.tile.view(-1)[: rgb.size] = torch.from_numpy(rgb).reshape(-1)
     img = tg.gather()
     if rank == 0:
         np.save(out_path, img.numpy())
@@ -120,10 +121,11 @@ def test_tile_cols_partition_and_pixel_assembly(band_log2):
         idx = pixel_assembly_index(world, H, W, band_log2=band_log2).tolist()
         cm = rows_max(world, W, band_log2)
         assert len(idx) == H * W and len(set(idx)) == H * W and max(idx) < world * H * cm
-        for k in range(world):  # pixel (y, x) of rank k's tile column j lands at x
-            for j, x in enumerate(tile_image_cols(k, world, W, band_log2)):
+        for k in range(world):  # pixel (y, j) of rank k's tile (row pitch: its own width) lands at x
+            mine = tile_image_cols(k, world, W, band_log2)
+            for j, x in enumerate(mine):
                 for y in range(H):
-                    assert idx[y * W + x] == (k * H + y) * cm + j
+                    assert idx[y * W + x] == k * H * cm + y * len(mine) + j
 
 
 def test_column_tiles_render_the_image_columns():

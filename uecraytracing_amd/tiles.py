@@ -82,18 +82,20 @@ def rank_tile(rank: int, world: int, height: int, width: int, deal: str = DEAL) 
 
 def pixel_assembly_index(world: int, height: int, width: int, device=None,
                          band_log2: int = COL_BAND_LOG2):
-    """Column dealing: image pixel (y, x) is pixel (y, j) of rank (x // C) % world's padded tile
-    (height x cols_max), the tiles stacked rank after rank; flattened pixel indices."""
+    """Column dealing: image pixel (y, x) is pixel (y, j) of rank r = (x // C) % world's tile.  A
+    rank's tile is height x its own width w_r, written contiguously (row pitch w_r, as the C-ABI
+    writes it) at the start of its height x cols_max slot; the slots are stacked rank after rank.
+    Flattened pixel indices."""
     import torch
     cm = rows_max(world, width, band_log2)
-    col_src = [0] * width
+    rank_of, j_of, w_of = [0] * width, [0] * width, [0] * width
     for r in range(world):
-        for j, x in enumerate(tile_image_cols(r, world, width, band_log2)):
-            col_src[x] = (r, j)
-    rank_of = torch.tensor([c[0] for c in col_src], dtype=torch.int64)
-    j_of = torch.tensor([c[1] for c in col_src], dtype=torch.int64)
+        cols = tile_image_cols(r, world, width, band_log2)
+        for j, x in enumerate(cols):
+            rank_of[x], j_of[x], w_of[x] = r, j, len(cols)
+    rank_of, j_of, w_of = (torch.tensor(v, dtype=torch.int64) for v in (rank_of, j_of, w_of))
     y = torch.arange(height, dtype=torch.int64)[:, None]
-    idx = (rank_of[None, :] * height + y) * cm + j_of[None, :]
+    idx = rank_of[None, :] * (height * cm) + y * w_of[None, :] + j_of[None, :]
     return idx.reshape(-1).to(device)
 
 
@@ -110,7 +112,8 @@ class TileGather:
             band_log2 = COL_BAND_LOG2 if deal == "cols" else BAND_LOG2
         self.rank, self.world, self.height, self.width = rank, world, height, width
         self.deal = deal if world > 1 else "rows"
-        if self.deal == "cols":  # tile: every row, cols_max columns (band_log2: the column bands)
+        if self.deal == "cols":  # tile: every row, cols_max columns (band_log2: the column bands);
+            # the render writes its height x (own width) pixels contiguously from the start
             self.rm, self.cm = height, rows_max(world, width, band_log2)
         else:
             self.rm, self.cm = rows_max(world, height, band_log2), width
