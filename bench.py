@@ -167,10 +167,11 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf, deal):
 
 
 def rank_tiles(ren, stream, seed0, frame_ms, deal):
-    """The N-GPU bound on this GPU: every rank's row tile of the N-way
-    split rendered ALONE (ms per call over 4 back-to-back calls after a warm one, HIP events on the
-    bench stream: the per-rank steps of the N-GPU bench), for config 3 at N = 2, 4, 8 and config 4's
-    eight 270-row tiles.  The slowest tile bounds the N-GPU step before the gather;
+    """The N-GPU bound on this GPU: every rank's tile of the N-way
+    split under `deal` (8-column bands or single rows, tiles.py) rendered ALONE (ms per call over 4
+    back-to-back calls after a warm one, HIP events on the bench stream: the per-rank steps of the
+    N-GPU bench), for config 3 at N = 2, 4, 8 and config 4's eight tiles, and the other dealing at
+    N = 8 for comparison.  The slowest tile bounds the N-GPU step before the gather;
     `speedup_bound` = the single-GPU frame (the contract line's ms per step for config 3; the
     same back-to-back timing of whole config-4 frames) / the slowest tile."""
     import torch

@@ -4,7 +4,7 @@ Bit-exact throughout: RGB8 bytes AND the per-pixel float64 sums before to_color3
   * reference-generated goldens (tests/golden, from /root/reference via oracle/_ref)
   * extension scenes (dielectric / fuzz / thin lens: parity unpinned vs the reference) against
     the oracle restatement
-  * row tiles (the multi-GPU partition), repeated calls, async into device memory
+  * row and column tiles (the multi-GPU partitions), repeated calls, async into device memory
   * the headline configuration's geometry at full size on a strided row subset
 """
 import numpy as np
@@ -178,7 +178,7 @@ def test_row_tiles_reassemble(ren):
 
 
 def test_banded_row_tiles_reassemble(ren):
-    """Bands of 2^k rows dealt cyclically (the N-GPU split of bench.py / tiles.py), including a
+    """Bands of 2^k rows dealt cyclically (bench.py --deal rows / tiles.py), including a
     partial last band: the tiles reassemble into the reference golden image bit for bit."""
     from uecraytracing_amd.tiles import tile_image_rows, tile_rows
     e = next(c for c in MAN["cases"] if c["name"] == "mixed12_96x54x16_d50_s404")

@@ -127,6 +127,11 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #ifndef YK_F32_SLOW_FOLD
 #define YK_F32_SLOW_FOLD 0
 #endif
+// FP32: the visit without the slow-axis read and FMAs for waves none of whose rays has a slow
+// axis (a wave-uniform branch)
+#ifndef YK_F32_SLOW_SPLIT
+#define YK_F32_SLOW_SPLIT 1
+#endif
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
 // Spheres per BVH leaf the kernels' leaf code handles: the FP64 leaf test is loop-free for one
@@ -1447,6 +1452,7 @@ void yk_render_f32(KernelArgs ka) {
         const float s = __builtin_sqrtf(a) * ykbvh::kF32Cone;  // the cone's slope (>= kF32Cone |d|)
         const float tmin_lo = tmin * (1.0f - 0x1p-17f);
         float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
+        bool lane_slow = false;    // the ray has a slow axis (YK_F32_SLOW_SPLIT)
 #if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS_F32
         // The axes in the order (A, B, C), C the ray's slow axis when it has one (y, then x, then
         // z, as below; else z).  A slow axis has no far bound, so C's far-plane FMA — the same
@@ -1534,6 +1540,7 @@ void yk_render_f32(KernelArgs ka) {
               cl2 = f2{-(ok[k] * jl), -(ok[k] * jl)};
 #endif
               pl = pk[k] + 16;
+              lane_slow = true;
             }
           }
         }
@@ -1548,6 +1555,15 @@ void yk_render_f32(KernelArgs ka) {
         int32_t node = ka.bvh_root;
         int32_t* top = stk;
         const int32_t* const stk_cap = stk + ka.stack_cap * kBlk;
+        // A wave none of whose rays has a slow axis (the bound is then -inf on every lane) skips
+        // the slow-axis plane read and FMAs (YK_F32_SLOW_SPLIT: a wave-uniform branch; the same
+        // culling decisions either way)
+#if YK_F32_SLOW_SPLIT && YK_SLAB_PAIRS_F32 && !YK_F32_SLOW_FOLD
+        const bool wave_slow = __builtin_amdgcn_readfirstlane(__ballot(lane_slow) != 0 ? 1u : 0u) != 0;
+#else
+        (void)lane_slow;
+        const bool wave_slow = true;
+#endif
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
@@ -1579,7 +1595,6 @@ void yk_render_f32(KernelArgs ka) {
             const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
             const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
             const int4 ch = *(const int4*)(nodes + node + 144);
-            const f4 qsl = *(const f4*)(pl + node);
             bool hk[4];
 #if YK_SLAB_PAIRS_F32
             const f2 nx[2] = {slab_fma(qnx.xy, inx), slab_fma(qnx.zw, inx)};
@@ -1588,15 +1603,26 @@ void yk_render_f32(KernelArgs ka) {
             const f2 fy[2] = {slab_fma(qfy.xy, jfy), slab_fma(qfy.zw, jfy)};
             const f2 nz[2] = {slab_fma(qnz.xy, inz), slab_fma(qnz.zw, inz)};
             const f2 fz[2] = {slab_fma(qfz.xy, jfz), slab_fma(qfz.zw, jfz)};
-            const f2 sl[2] = {slab_fma(qsl.xy, jl2), slab_fma(qsl.zw, jl2)};
+            if (wave_slow) {
+              const f4 qsl = *(const f4*)(pl + node);
+              const f2 sl[2] = {slab_fma(qsl.xy, jl2), slab_fma(qsl.zw, jl2)};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const float tn = slab_max3(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]),
-                                         sl[k >> 1][k & 1], tmin_lo);
-              const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
-              hk[k] = tn <= tf;
+              for (int k = 0; k < 4; ++k) {
+                const float tn = slab_max3(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]),
+                                           sl[k >> 1][k & 1], tmin_lo);
+                const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
+                hk[k] = tn <= tf;
+              }
+            } else {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const float tn = slab_max(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]), tmin_lo);
+                const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
+                hk[k] = tn <= tf;
+              }
             }
 #else
+            const f4 qsl = *(const f4*)(pl + node);
             const f2 nx[2] = {__builtin_elementwise_fma(qnx.xy, inx, ncx), __builtin_elementwise_fma(qnx.zw, inx, ncx)};
             const f2 fx[2] = {__builtin_elementwise_fma(qfx.xy, jfx, fcx), __builtin_elementwise_fma(qfx.zw, jfx, fcx)};
             const f2 ny[2] = {__builtin_elementwise_fma(qny.xy, iny, ncy), __builtin_elementwise_fma(qny.zw, iny, ncy)};
