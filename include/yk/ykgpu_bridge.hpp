@@ -23,6 +23,7 @@
 #include <iomanip>
 #include <ostream>
 #include <stdexcept>
+#include <initializer_list>
 #include <string>
 #include <tuple>
 #include <type_traits>
@@ -199,6 +200,32 @@ inline std::vector<int> devices_from_env(const char* var = "YKGPU_DEVICES") {
       throw error(YK_ERR_INVALID, std::string(var) + ": device " + std::to_string(k) + " of " + v + " does not exist (" +
                                       std::to_string(n) + " devices)");
   return d;
+}
+
+// The drop-in's render modes from the environment (all optional; unset = render() as the
+// constexpr build computes it):
+//   YKGPU_SEED      "counter" (seed0 + (y*W + x)*spp + s, source.cpp:154-158) or "random_device"
+//                   (the runtime build's per-sample std::random_device seeding, source.cpp:159:
+//                   a fresh key per call, not reproducible)
+//   YKGPU_PRECISION "fp64" or "fp32" (render<float>, source.cpp:98-99)
+//   YKGPU_RNG       "mt19937" or "xor128" (yk::xor128 as the per-sample engine)
+inline render_options options_from_env() {
+  render_options o;
+  auto pick = [](const char* var, std::initializer_list<std::pair<const char*, uint32_t>> names,
+                 uint32_t dflt) -> uint32_t {
+    const char* e = std::getenv(var);
+    if (!e || !*e) return dflt;
+    std::string all;
+    for (const auto& n : names) {
+      if (std::string(e) == n.first) return n.second;
+      all += std::string(all.empty() ? "" : ", ") + n.first;
+    }
+    throw error(YK_ERR_INVALID, std::string(var) + ": " + e + " is not one of " + all);
+  };
+  o.seed_mode = pick("YKGPU_SEED", {{"counter", YK_SEED_COUNTER}, {"random_device", YK_SEED_RANDOM_DEVICE}}, o.seed_mode);
+  o.precision = pick("YKGPU_PRECISION", {{"fp64", YK_PRECISION_FP64}, {"fp32", YK_PRECISION_FP32}}, o.precision);
+  o.rng = pick("YKGPU_RNG", {{"mt19937", YK_RNG_MT19937}, {"xor128", YK_RNG_XOR128}}, o.rng);
+  return o;
 }
 
 // The render loop of source.cpp:122-172 on the GPU: one device context, or — given several

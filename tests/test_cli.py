@@ -237,6 +237,51 @@ def test_patched_reference_rejects_a_bad_device_list(tmp_path):
         assert not (tmp_path / "o.png").exists()
 
 
+def test_patched_reference_rejects_unknown_render_modes(tmp_path):
+    """YKGPU_SEED / YKGPU_PRECISION / YKGPU_RNG (the bridge's options_from_env) that name no mode
+    fail loudly before any device is touched."""
+    need(PATCHED["_16x2"])
+    for var, bad in (("YKGPU_SEED", "urandom"), ("YKGPU_PRECISION", "fp16"), ("YKGPU_RNG", "pcg")):
+        r = subprocess.run([PATCHED["_16x2"], "o.png"], cwd=tmp_path, capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, **{var: bad}))
+        assert r.returncode != 0
+        assert var in r.stderr and bad in r.stderr, r.stderr
+        assert not (tmp_path / "o.png").exists()
+
+
+@pytest.mark.gpu
+def test_patched_reference_render_modes_from_the_environment(tmp_path):
+    """The drop-in's other modes through the reference's own main: YKGPU_PRECISION=fp32
+    (render<float>) and YKGPU_RNG=xor128 give the library's images of those modes byte for byte
+    (themselves pinned to the reference by goldens); YKGPU_SEED=random_device is the runtime
+    build's per-sample std::random_device seeding (source.cpp:159): two runs differ from each
+    other and from the counter-seeded image."""
+    need(PATCHED["_200x8"])
+    from uecraytracing_amd.records import PRECISION_FP32, RNG_XOR128
+    import refscenes
+    with yk.Renderer(0) as r:
+        r.set_scene(refscenes.ref4(), refscenes.reference_camera())
+        for var, val, kw in (("YKGPU_PRECISION", "fp32", {"precision": PRECISION_FP32}),
+                             ("YKGPU_RNG", "xor128", {"rng": RNG_XOR128})):
+            want = r.render(yk.make_params(200, 112, 8, 50, 404, **kw))
+            out = subprocess.run([PATCHED["_200x8"], f"{val}.png"], cwd=tmp_path, capture_output=True, text=True,
+                                 timeout=300, env=dict(os.environ, **{var: val}))
+            assert out.returncode == 0, out.stderr
+            rgb, W, H = golden_data.png_rgb(str(tmp_path / f"{val}.png"))
+            assert (W, H) == (200, 112) and rgb == want.tobytes()
+    imgs = []
+    for k in range(2):
+        out = subprocess.run([PATCHED["_200x8"], f"rd{k}.png"], cwd=tmp_path, capture_output=True, text=True,
+                             timeout=300, env=dict(os.environ, YKGPU_SEED="random_device"))
+        assert out.returncode == 0, out.stderr
+        rgb, W, H = golden_data.png_rgb(str(tmp_path / f"rd{k}.png"))
+        assert (W, H) == (200, 112)
+        imgs.append(rgb)
+    e = next(c for c in MAN["cases"] if c["name"] == "ref4_200x112x8_d50_s404")
+    assert imgs[0] != imgs[1]
+    assert all(golden_data.sha(np.frombuffer(x, np.uint8)) != e["rgb_sha256"] for x in imgs)
+
+
 @pytest.mark.gpu
 def test_patched_reference_console_matches_runtime_build(tmp_path):
     """-v / -l 2: the unmodified runtime build's lines do not depend on its random seeds, so the

@@ -280,6 +280,37 @@ def test_async_into_device_memory(ren):
     np.testing.assert_array_equal(out.cpu().numpy(), golden_data.rgb(e))
 
 
+def test_back_to_back_calls_equal_a_synced_call(ren):
+    """Calls enqueued while the previous one still runs overlap it (rings by global
+    launch number, launches at kmax from the first) — in FP64, FP32 and xor128, with a call of
+    another shape between them (which must not overlap): every output equals the synced render of
+    its params, and the golden where there is one."""
+    torch = pytest.importorskip("torch")
+    ren.set_scene(refscenes.mixed12(), refscenes.reference_camera())
+    e = next(c for c in MAN["cases"] if c["name"] == "mixed12_96x54x16_d50_s404")
+    ps = [make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"]),
+          make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"]),
+          make_params(e["W"], e["H"], 24, e["depth"], e["seed0"], rows=(3, 20, 2)),  # another shape
+          make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"]),
+          make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], precision=PRECISION_FP32),
+          make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], precision=PRECISION_FP32),
+          make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], rng=RNG_XOR128),
+          make_params(e["W"], e["H"], e["spp"], e["depth"], e["seed0"], rng=RNG_XOR128)]
+    want = [ren.render(p) for p in ps]
+    np.testing.assert_array_equal(want[0], golden_data.rgb(e))
+    outs = [torch.zeros((p.row_count, p.tile_width(), 3), dtype=torch.uint8, device="cuda:0") for p in ps]
+    stream = torch.cuda.Stream()
+    for rep in range(2):
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()  # (the zeroing ran on torch's stream)
+        for p, o in zip(ps, outs):  # no synchronisation between the calls
+            ren.render_async(p, o.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        for w, o in zip(want, outs):
+            np.testing.assert_array_equal(o.cpu().numpy(), w)
+
+
 def test_headline_geometry_full_size_rows(ren):
     """1920x1080x512 on the ~488-sphere final scene: rows 0 and 539 bit-exact vs the oracle."""
     arr, cam = yk.build_scene("final", 42)
