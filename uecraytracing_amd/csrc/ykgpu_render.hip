@@ -128,9 +128,11 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #define YK_F32_SLOW_FOLD 0
 #endif
 // FP32: the visit without the slow-axis read and FMAs for waves none of whose rays has a slow
-// axis (a wave-uniform branch)
+// axis (a wave-uniform branch in the visit): slower, 191.3 -> 198.5 ms (profiles/r04_ab/f32/);
+// off.  (A version with the loop in two instances through a generic lambda kept the candidate
+// list in scratch: 224 ms.)
 #ifndef YK_F32_SLOW_SPLIT
-#define YK_F32_SLOW_SPLIT 1
+#define YK_F32_SLOW_SPLIT 0
 #endif
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
