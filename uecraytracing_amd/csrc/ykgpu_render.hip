@@ -5,11 +5,13 @@
 // samples → to_color3b) and the recursion of yk/raytracer.hpp:19-37.
 //
 // Execution model:
-//   * a render call is a sequence of LAUNCHES of K samples per pixel (8, 32, then at most
-//     kLaunchSpp = 32; 1920x1080x512: 8, 15 x 32, 24).  Per launch: yk_mt_warmup (second
-//     stream: every sample's mt19937 seeding walk and, for the FP64 kernel, its start draws —
-//     jitter and lens — as a StartRec), yk_render_persistent (the paths), yk_reduce_samples (the
-//     reference's strictly sequential per-pixel sum and to_color3b, third stream).
+//   * a render call is a sequence of LAUNCHES of K samples per pixel (4, 8, 16, then at most
+//     kmax = kLaunchSpp = 32 for the frame: 1920x1080x512 is 4, 8, 16, 14 x 32, 18, 18; a call
+//     enqueued while the previous one still runs: 16 x 32).  Per launch: yk_mt_warmup (second
+//     stream: every sample's mt19937 seeding walk and its start draws — jitter and lens — and
+//     camera ray, as a StartRec), yk_render_persistent (the paths, on one of two top-priority
+//     streams), yk_reduce_samples (the reference's strictly sequential per-pixel sum and
+//     to_color3b, third stream).  Back-to-back calls overlap (launches numbered across calls).
 //   * yk_render_persistent is one persistent grid of 768-thread workgroups, one per CU, with
 //     the scene (BVH, geometry and material tables) in LDS, over SAMPLE SLOTS: a lane runs one path at a
 //     time, one SEGMENT (closest hit + scatter) per trip round the loop, writes the sample's
