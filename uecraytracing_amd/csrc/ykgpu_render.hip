@@ -2302,8 +2302,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const bool f32 = p->precision == YK_PRECISION_FP32;
   const bool x128 = p->rng == YK_RNG_XOR128;  // no warm-ups, no MT scratch
   const DevTree& tree = f32 ? ctx->t32 : ctx->t64;
-  // FP64 mt19937: two paths per lane (yk_render_dual) unless YKGPU_DUAL=0 or the one-lane
-  // diagnostic (the single-path counting instance's)
+  // FP64 mt19937 with YKGPU_DUAL=1 (A/B): two paths per lane (yk_render_dual), except for the
+  // one-lane diagnostic (the single-path counting instance's)
   const bool dual = !f32 && !x128 && !(p->flags & YK_FLAG_ONE_LANE) && dual_enabled();
   const DevTree::Plan& plan = tree.plan[dual ? 2 : (x128 ? 1 : 0)];
   const int grid = plan.grid, block = dual ? kDualBlock : block_of(x128);
@@ -2329,8 +2329,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // per sample slot, kLaunchBytes per launch); a short remainder is folded into the launches before
   // it (1920x1080x512: 4, 8, 16, 14 x 32, 18, 18 = 19 launches).  The first render waits only for
   // a 4-sample warm-up, and each next warm-up, twice the one before, finishes under the render
-  // before it (see kSchedGrow).  Each launch ends with the tail of its longest paths (~1 ms), but
-  // launches alternate between two streams, so that drain overlaps the next launch: many
+  // before it (see kSchedGrow).  Each launch ends with the tail of its longest paths (~0.1-0.2 ms
+  // of partly idle CUs), but launches alternate between two streams, so that drain overlaps the
+  // next launch: many
   // mid-sized launches beat a few large ones.  Independent of the image size, which matters
   // for the per-rank tiles of N GPUs.
   const uint32_t nps = ctx->order_slots;  // processing slots (>= pixels)
