@@ -104,14 +104,17 @@ class TileGather:
     the timed loop allocates nothing)."""
 
     def __init__(self, rank: int, world: int, height: int, width: int, device, band_log2: int | None = None,
-                 deal: str = "rows"):
+                 deal: str = "rows", collective: bool | None = None):
+        """collective: run the collective and the de-interleave (default: world > 1; True at
+        world 1 exercises the N-rank branch on one device, tests/test_gpu_tiles_rccl.py)."""
         import torch
         if deal not in ("rows", "cols"):
             raise ValueError(f"deal must be 'rows' or 'cols', not {deal!r}")
         if band_log2 is None:
             band_log2 = COL_BAND_LOG2 if deal == "cols" else BAND_LOG2
         self.rank, self.world, self.height, self.width = rank, world, height, width
-        self.deal = deal if world > 1 else "rows"
+        self.collective = world > 1 if collective is None else bool(collective)
+        self.deal = deal if self.collective else "rows"
         if self.deal == "cols":  # tile: every row, cols_max columns (band_log2: the column bands);
             # the render writes its height x (own width) pixels contiguously from the start
             self.rm, self.cm = height, rows_max(world, width, band_log2)
@@ -120,7 +123,7 @@ class TileGather:
         self.tile = torch.zeros((self.rm, self.cm, 3), dtype=torch.uint8, device=device)
         self.image = torch.empty((height, width, 3), dtype=torch.uint8, device=device)
         self.gathered = (torch.empty((world, self.rm, self.cm, 3), dtype=torch.uint8, device=device)
-                         if rank == 0 and world > 1 else None)
+                         if rank == 0 and self.collective else None)
         self.index = (pixel_assembly_index(world, height, width, device, band_log2) if self.deal == "cols"
                       else assembly_index(world, height, device, band_log2))
 
@@ -128,7 +131,7 @@ class TileGather:
         """Collective + de-interleave; after it, rank 0's self.image holds the whole image."""
         import torch
         import torch.distributed as dist
-        if self.world == 1:
+        if not self.collective:
             self.image.copy_(self.tile[: self.height])
             return self.image
         if self.tile.is_cuda and dist.get_backend() == "gloo":
