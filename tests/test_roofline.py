@@ -97,7 +97,10 @@ def test_rocprof_union_agrees_with_bench_launch_ms():
         pytest.skip("no kernel trace union for the latest bench")
     b = json.load(open(bench))
     u = json.load(open(union))
-    assert abs(u["union_per_dispatch_ms"] - b["roofline"]["launch_ms"]) / b["roofline"]["launch_ms"] < 0.05
+    # round 4 on, the traced run mixes synced calls (launches of 4-32 spp) and back-to-back ones:
+    # compare per 32-spp launch equivalent (tools/kernel_union.py)
+    per = u.get("union_per_launch_equiv_ms", u["union_per_dispatch_ms"])
+    assert abs(per - b["roofline"]["launch_ms"]) / b["roofline"]["launch_ms"] < 0.05
 
 
 def test_peak_falls_back_to_the_datasheet_without_the_ubench_file(tmp_path):

@@ -6,6 +6,11 @@ twice.  This reports, for the dispatches whose name contains the substring: the 
 span (what --stats prints), the UNION of the spans, and union / dispatches — the figure bench.py
 divides by (`roofline.launch_ms`).
 usage: python tools/kernel_union.py <run_kernel_trace.csv> [kernel-substring[|substring...]] [out.json]
+                                    [spp_total spp_per_launch]
+With spp_total (every sample per pixel the traced run rendered with this kernel) and the bench's
+launch size, also union_per_launch_equiv_ms = union / (spp_total / spp_per_launch): the traced
+run mixes synced calls (launches of 4, 8, 16, 32 spp) and back-to-back ones (32 each), so this is
+the figure comparable with the bench's per-32-spp launch_ms.
 Several substrings ('|'-separated) take the union of all their dispatches (kernels that share a
 launch); "launches" = the dispatches of the LAST substring (one per launch).
 """
@@ -38,6 +43,10 @@ def main():
            "avg_span_ms": spans / len(iv) / 1e6, "union_ms": union / 1e6,
            "union_per_dispatch_ms": union / max(1, launches) / 1e6,
            "overlap_fraction_of_spans": 1 - union / spans}
+    if len(sys.argv) > 5:
+        spp_total, per = float(sys.argv[4]), float(sys.argv[5])
+        out["spp_total"], out["spp_per_launch"] = spp_total, per
+        out["union_per_launch_equiv_ms"] = union / (spp_total / per) / 1e6
     js = json.dumps(out, indent=1)
     if len(sys.argv) > 3:
         open(sys.argv[3], "w").write(js + "\n")
