@@ -123,19 +123,8 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #ifndef YK_SLAB_PAIRS_F32
 #define YK_SLAB_PAIRS_F32 1
 #endif
-// FP32 visit: the slow-axis lower bound taken from the slow axis' own far-plane read (its far
-// bound is void there) instead of a seventh plane read: one read and two packed
-// FMAs fewer per visit, but slower (512 spp 195.3 -> 199.0 ms, profiles/r04_ab/f32/): off
-#ifndef YK_F32_SLOW_FOLD
-#define YK_F32_SLOW_FOLD 0
-#endif
-// FP32: the visit without the slow-axis read and FMAs for waves none of whose rays has a slow
-// axis (a wave-uniform branch in the visit): slower, 191.3 -> 198.5 ms (profiles/r04_ab/f32/);
-// off.  (A version with the loop in two instances through a generic lambda kept the candidate
-// list in scratch: 224 ms.)
-#ifndef YK_F32_SLOW_SPLIT
-#define YK_F32_SLOW_SPLIT 0
-#endif
+// (Tried and removed in round 4, DESIGN.md §4.1: the FP32 slow-axis bound folded into the slow
+// axis' far-plane FMA, +2.3%; the slow-axis read skipped in waves without a slow-axis ray, +3.8%.)
 using DevNode = ykbvh::WideNode;  // 4-wide BVH nodes (yk_bvh.hpp)
 constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp builds), [24..31]: work
 // Spheres per BVH leaf the kernels' leaf code handles: the FP64 leaf test is loop-free for one
@@ -1456,59 +1445,6 @@ void yk_render_f32(KernelArgs ka) {
         const float s = __builtin_sqrtf(a) * ykbvh::kF32Cone;  // the cone's slope (>= kF32Cone |d|)
         const float tmin_lo = tmin * (1.0f - 0x1p-17f);
         float ustar_f = INFINITY;  // T (1 + 2^-18): every box that may hold a root <= T passes
-        bool lane_slow = false;    // the ray has a slow axis (YK_F32_SLOW_SPLIT)
-#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS_F32
-        // The axes in the order (A, B, C), C the ray's slow axis when it has one (y, then x, then
-        // z, as below; else z).  A slow axis has no far bound, so C's far-plane FMA — the same
-        // quad the slow-axis bound reads — serves as the far bound when the ray has no slow axis
-        // and as the slow-axis lower bound when it has one; two clamps route it (v_med3):
-        //   X = med3(fC, ulo, U') = slow ? U' : min(fC, U')    (ulo = slow ? U' : -inf)
-        //   Y = med3(fC, tmin', H) = slow ? max(fC, tmin') : tmin'   (H = slow ? +inf : tmin')
-        //   tf = min3(fA, fB, X), tn = max(max3(nA, nB, nC), Y)
-        // which are the separate-read test's tf and tn (the same culling decisions, the same
-        // traversal): one 16-byte plane read and two packed FMAs fewer per visit.
-        f2 inA, ncA, jfA, fcA, inB, ncB, jfB, fcB, inC, ncC, jfC, fcC;
-        const char *pA, *pB, *pC;
-        float ulo_sel, hi_sel;  // the ray has a slow axis: (+inf, +inf); else (-inf, tmin')
-        {
-          const float dk[3] = {d.x, d.y, d.z}, ok[3] = {o.x, o.y, o.z};
-          float in[3], nc[3], jf[3], fc[3];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {  // cone_axis's operands
-            const float sg = dk[k] < 0.0f ? -s : s;
-            in[k] = __builtin_amdgcn_rcpf(dk[k] + sg);
-            nc[k] = -(ok[k] * in[k]);
-            const bool far = fabsf(dk[k]) >= kF32FarAt * s;
-            jf[k] = far ? __builtin_amdgcn_rcpf(dk[k] - sg) * (1.0f + 0x1p-17f) : 0.0f;
-            fc[k] = far ? -(ok[k] * jf[k]) : INFINITY;
-          }
-          const float slow = s * kF32SlowAt;
-          const bool sx = fabsf(d.x) < slow, sy = fabsf(d.y) < slow, sz = fabsf(d.z) < slow;
-          const int kc = sy ? 1 : (sx ? 0 : 2), ka_ = kc == 0 ? 1 : 0, kb_ = kc == 2 ? 1 : 2;
-          // (selects, not indexing: a run-time index would put the arrays in scratch)
-          const auto pick = [](const float* v, int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : v[2]); };
-          float jc = pick(jf, kc), cc = pick(fc, kc);
-          if (sx || sy || sz) {  // C's far FMA gives the slow-axis bound: (plane - o) / (d - s sign d)
-            const float dc = pick(dk, kc);
-            jc = __builtin_amdgcn_rcpf(dc - (dc < 0.0f ? -s : s));
-            cc = -(pick(ok, kc) * jc);
-          }
-          const float ina = pick(in, ka_), nca = pick(nc, ka_), jfa = pick(jf, ka_), fca = pick(fc, ka_);
-          const float inb = pick(in, kb_), ncb = pick(nc, kb_), jfb = pick(jf, kb_), fcb = pick(fc, kb_);
-          const float inc = pick(in, kc), ncc = pick(nc, kc);
-          inA = f2{ina, ina}, ncA = f2{nca, nca}, jfA = f2{jfa, jfa}, fcA = f2{fca, fca};
-          inB = f2{inb, inb}, ncB = f2{ncb, ncb}, jfB = f2{jfb, jfb}, fcB = f2{fcb, fcb};
-          inC = f2{inc, inc}, ncC = f2{ncc, ncc}, jfC = f2{jc, jc}, fcC = f2{cc, cc};
-          // each axis' (near x4, far x4) plane quads of the ray's direction sign in a WideNode
-          const uint32_t ox = d.x < 0.0f ? 16u : 0u, oy = d.y < 0.0f ? 64u : 48u, oz = d.z < 0.0f ? 112u : 96u;
-          pA = nodes + (ka_ == 0 ? ox : oy);
-          pB = nodes + (kb_ == 1 ? oy : oz);
-          pC = nodes + (kc == 0 ? ox : (kc == 1 ? oy : oz));
-          ulo_sel = (sx || sy || sz) ? INFINITY : -INFINITY;
-          hi_sel = (sx || sy || sz) ? INFINITY : tmin_lo;
-        }
-        float ulo = fminf(ustar_f, ulo_sel);
-#else
         f2 inx, ncx, jfx, fcx, iny, ncy, jfy, fcy, inz, ncz, jfz, fcz;
         cone_axis(d.x, o.x, s, inx, ncx, jfx, fcx);
         cone_axis(d.y, o.y, s, iny, ncy, jfy, fcy);
@@ -1544,11 +1480,9 @@ void yk_render_f32(KernelArgs ka) {
               cl2 = f2{-(ok[k] * jl), -(ok[k] * jl)};
 #endif
               pl = pk[k] + 16;
-              lane_slow = true;
             }
           }
         }
-#endif
         // U*: proven upper bound of the minimum root (culls with ustar_f = U* (1 + 2^-18)); the
         // candidate list (tuple index, lower bound) as in the FP64 kernel, nc = 5 on overflow
         const float ia = __builtin_amdgcn_rcpf(a);  // a in [2^-60, 2^60] here
@@ -1559,42 +1493,11 @@ void yk_render_f32(KernelArgs ka) {
         int32_t node = ka.bvh_root;
         int32_t* top = stk;
         const int32_t* const stk_cap = stk + ka.stack_cap * kBlk;
-        // A wave none of whose rays has a slow axis (the bound is then -inf on every lane) skips
-        // the slow-axis plane read and FMAs (YK_F32_SLOW_SPLIT: a wave-uniform branch; the same
-        // culling decisions either way)
-#if YK_F32_SLOW_SPLIT && YK_SLAB_PAIRS_F32 && !YK_F32_SLOW_FOLD
-        const bool wave_slow = __builtin_amdgcn_readfirstlane(__ballot(lane_slow) != 0 ? 1u : 0u) != 0;
-#else
-        (void)lane_slow;
-        const bool wave_slow = true;
-#endif
         for (;;) {
           if (node >= 0) {
             if (kCount) ++n_node;
             YK_STAMP_NODE_ITERATION(lane);
             // the FP64 kernel's visit (same planes, margins and visit order), the cone's operands
-#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS_F32
-            const f4 qnA = *(const f4*)(pA + node), qfA = *(const f4*)(pA + node + 16);
-            const f4 qnB = *(const f4*)(pB + node), qfB = *(const f4*)(pB + node + 16);
-            const f4 qnC = *(const f4*)(pC + node), qfC = *(const f4*)(pC + node + 16);
-            const int4 ch = *(const int4*)(nodes + node + 144);
-            bool hk[4];
-            const f2 nA[2] = {__builtin_elementwise_fma(qnA.xy, inA, ncA), __builtin_elementwise_fma(qnA.zw, inA, ncA)};
-            const f2 fA[2] = {__builtin_elementwise_fma(qfA.xy, jfA, fcA), __builtin_elementwise_fma(qfA.zw, jfA, fcA)};
-            const f2 nB[2] = {__builtin_elementwise_fma(qnB.xy, inB, ncB), __builtin_elementwise_fma(qnB.zw, inB, ncB)};
-            const f2 fB[2] = {__builtin_elementwise_fma(qfB.xy, jfB, fcB), __builtin_elementwise_fma(qfB.zw, jfB, fcB)};
-            const f2 nC[2] = {__builtin_elementwise_fma(qnC.xy, inC, ncC), __builtin_elementwise_fma(qnC.zw, inC, ncC)};
-            const f2 fC[2] = {__builtin_elementwise_fma(qfC.xy, jfC, fcC), __builtin_elementwise_fma(qfC.zw, jfC, fcC)};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const float c = fC[k >> 1][k & 1];
-              const float x = __builtin_amdgcn_fmed3f(c, ulo, ustar_f);    // C as far bound, or U'
-              const float y = __builtin_amdgcn_fmed3f(c, tmin_lo, hi_sel);  // C as slow bound, or tmin'
-              const float tn = fmaxf(fmaxf(fmaxf(nA[k >> 1][k & 1], nB[k >> 1][k & 1]), nC[k >> 1][k & 1]), y);
-              const float tf = fminf(fminf(fA[k >> 1][k & 1], fB[k >> 1][k & 1]), x);
-              hk[k] = tn <= tf;
-            }
-#else
             const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
             const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
             const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
@@ -1607,23 +1510,14 @@ void yk_render_f32(KernelArgs ka) {
             const f2 fy[2] = {slab_fma(qfy.xy, jfy), slab_fma(qfy.zw, jfy)};
             const f2 nz[2] = {slab_fma(qnz.xy, inz), slab_fma(qnz.zw, inz)};
             const f2 fz[2] = {slab_fma(qfz.xy, jfz), slab_fma(qfz.zw, jfz)};
-            if (wave_slow) {
-              const f4 qsl = *(const f4*)(pl + node);
-              const f2 sl[2] = {slab_fma(qsl.xy, jl2), slab_fma(qsl.zw, jl2)};
+            const f4 qsl = *(const f4*)(pl + node);
+            const f2 sl[2] = {slab_fma(qsl.xy, jl2), slab_fma(qsl.zw, jl2)};
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const float tn = slab_max3(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]),
-                                           sl[k >> 1][k & 1], tmin_lo);
-                const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
-                hk[k] = tn <= tf;
-              }
-            } else {
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const float tn = slab_max(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]), tmin_lo);
-                const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
-                hk[k] = tn <= tf;
-              }
+            for (int k = 0; k < 4; ++k) {
+              const float tn = slab_max3(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]),
+                                         sl[k >> 1][k & 1], tmin_lo);
+              const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
+              hk[k] = tn <= tf;
             }
 #else
             const f4 qsl = *(const f4*)(pl + node);
@@ -1642,7 +1536,6 @@ void yk_render_f32(KernelArgs ka) {
               const float tf = fminf(fminf(fminf(fx[k >> 1][k & 1], fy[k >> 1][k & 1]), fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
-#endif
 #endif
             asm volatile("" ::"v"(ch.x), "v"(ch.y), "v"(ch.z), "v"(ch.w));
             if (hk[0] || hk[1] || hk[2] || hk[3]) {
@@ -1694,9 +1587,6 @@ void yk_render_f32(KernelArgs ka) {
               if (ub < ustar) {
                 ustar = ub;
                 ustar_f = ub * (1.0f + 0x1p-18f);
-#if YK_F32_SLOW_FOLD && !YK_SLAB_PAIRS_F32
-                ulo = fminf(ustar_f, ulo_sel);
-#endif
               }
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
