@@ -1,5 +1,5 @@
 """Per-phase wave-cycle shares from the stamp build (yk_stamps.hpp, -DYK_STAMPS=1; diagnostic only).
-usage: [PREC=1] [ROWS=b:c:s] python tools/phases.py [scene [spp]]   (PREC=1: render<float>)"""
+usage: [PREC=1] [ROWS=b:c:s] [DEPTH=n] python tools/phases.py [scene [spp]]   (PREC=1: render<float>; DEPTH: max_depth, 50)"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import uecraytracing_amd as yk
@@ -11,7 +11,7 @@ prec = int(os.environ.get("PREC", "0"))
 with yk.Renderer(0) as r:
     r.set_scene(arr, cam)
     rows = tuple(int(v) for v in os.environ["ROWS"].split(":")) if os.environ.get("ROWS") else None
-    p = make_params(1920, None, spp, 50, 404, rows=rows, flags=1, precision=prec)
+    p = make_params(1920, None, spp, int(os.environ.get("DEPTH", "50")), 404, rows=rows, flags=1, precision=prec)
     r.render(p); r.render(p)
     st = r.stats()
     pc = st["phase_cycles"]

@@ -2041,6 +2041,11 @@ static_assert(kLaunchBytes / (8 * kColStride) * 4 < (1ull << 32), "4 * slot must
 #define YK_LAUNCH_SPP 32
 #endif
 constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
+// ... or spp / kLaunchesPerCall when that is more (a long call: launch())
+#ifndef YK_LAUNCHES_PER_CALL
+#define YK_LAUNCHES_PER_CALL 32
+#endif
+constexpr uint32_t kLaunchesPerCall = YK_LAUNCHES_PER_CALL;
 // ... and at least kLaunchSlots sample slots per launch when the tile is small: a launch has a
 // fixed cost (its warm-up, the ramp of its persistent grid, a reduce), so a thin row tile needs
 // more samples per launch (8-way tile of 1920x1080x512, 135 rows: 31.5 ms at 32 spp per launch,
@@ -2234,8 +2239,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   uint64_t launch_slots = kLaunchSlots;  // (A/B knob: YKGPU_LAUNCH_SLOTS)
   if (const char* e = std::getenv("YKGPU_LAUNCH_SLOTS")) launch_slots = (uint64_t)std::max(1ll, std::atoll(e));
   const uint64_t slot_spp = (launch_slots + nps - 1) / nps;
-  uint64_t launch_spp = kLaunchSpp;  // (A/B knob: YKGPU_LAUNCH_SPP)
-  if (const char* e = std::getenv("YKGPU_LAUNCH_SPP")) launch_spp = (uint64_t)std::max(1, std::atoi(e));
+  // A long call takes longer launches: every launch pays a drain whose length is the longest path
+  // of its last samples, and many launches per call buy nothing once there are ~32 (config 5,
+  // 1920x1080x4096 at depth 200 on the glass scene: 32 spp per launch 1730 ms, 64 1631, 121 (the
+  // colour budget) 1589, with a warm ring of 2 1610; config 3's 512 spp stay at 32, where 64
+  // costs 5%; profiles/r04_ab/launch_size/).  The rings grow with the launch: config 5 holds
+  // ~64 GB (3 x 2.07M x 121 x 64 B of start records, 2 x 2.07M x 121 x 32 B of colours).
+  uint64_t launch_spp = std::max<uint64_t>(kLaunchSpp, spp / kLaunchesPerCall);
+  if (const char* e = std::getenv("YKGPU_LAUNCH_SPP")) launch_spp = (uint64_t)std::max(1, std::atoi(e));  // (A/B)
   const uint32_t kmax = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
                              std::max<uint64_t>({launch_spp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
