@@ -81,9 +81,21 @@ def pmc_facts(workload=None):
     if workload is not None and rec.get("workload") != workload:
         return None
     keep = ("source", "kernel", "workload", "mean_ms", "valu_pipe_util", "valu_lane_utilization",
-            "SQ_WAIT_ANY_frac", "SQ_WAIT_INST_ANY_frac", "hbm_bytes_per_launch",
+            "SQ_WAIT_ANY_frac", "SQ_WAIT_INST_ANY_frac", "hbm_bytes_per_launch", "hbm_bytes_per_sample",
             "fp64_flops_hw_per_launch")
     return {k: rec[k] for k in keep if k in rec}
+
+
+PMC_LANE_OPS = os.path.join(ROOT, "profiles", "pmc_lane_ops.json")
+
+
+def pmc_lane_ops():
+    """The committed reconciliation of the lane-op model with the PMC counters
+    (tools/lane_ops_reconcile.py), or None."""
+    if not os.path.exists(PMC_LANE_OPS):
+        return None
+    with open(PMC_LANE_OPS) as f:
+        return json.load(f)
 
 
 def other_configs(ren, stream, seed0, nthreads, peak_tf, deal):
@@ -352,6 +364,7 @@ def main():
     # union can exceed the step; the renders then run through the whole step period, which bounds
     # the per-step render time.
     busy_ms = tst["render_busy_ms"]
+    clamped = busy_ms > ms_per_step
     launch_ms = min(busy_ms, ms_per_step) / launches
     # the FP64 VALU peak measured on this chip (tools/ubench.hip → profiles/r03_ubench.jsonl)
     peak_tf, peak_ev = flops.fp64_valu_peak()
@@ -366,6 +379,36 @@ def main():
     workload = f"{args.scene}{args.scene_seed}_{W}x{H}x{spp}_d{depth}_n{world}"
     facts = pmc_facts(workload)
     traffic = facts.get("hbm_bytes_per_launch") if facts else None
+    # per SAMPLE, so that the ratio compares like with like (the PMC passes profile synced calls,
+    # whose launches are smaller on average than the bench's back-to-back ones)
+    traffic_ps = facts.get("hbm_bytes_per_sample") if facts else None
+    alg_ps = hbm_step / (pix_mine * spp)
+    # The VALU lane-op roofline of the path's whole work (flops.py: FP64 flops + the RNG's
+    # integer ops, by kernel): the seed walks (yk_mt_warmup) and the paths (yk_render_persistent)
+    # share every SIMD, so the STEP figure (both kernels' work over the step) is the path's; each
+    # kernel's own figure divides by its own per-launch span
+    costs, costs_src = flops.issue_costs()
+    lo = flops.lane_ops(st)
+    both = {k: lo["warmup"][k] + lo["render"][k] for k in lo["render"]}
+    per_l = lambda d: {k: v / launches for k, v in d.items()}
+    valu_ops = {
+        "render": dict(flops.lane_op_roofline(per_l(lo["render"]), launch_ms * 1e-3, costs),
+                       kernel="yk_render_persistent", per="launch", seconds_source="launch_ms"),
+        "warmup": dict(flops.lane_op_roofline(per_l(lo["warmup"]), tst["warmup_ms"] / launches * 1e-3, costs),
+                       kernel="yk_mt_warmup", per="launch",
+                       seconds_source="the step's warm-up HIP-event spans / launches"),
+        "step": dict(flops.lane_op_roofline(both, ms_per_step * 1e-3, costs), per="step",
+                     seconds_source="ms_per_step (both kernels share the SIMDs)"),
+        "issue_cycles_per_wave_instr": costs, "issue_cycles_source": costs_src,
+        "per_sample": {k: round(v / st["samples"], 2) for k, v in both.items()},
+        "counted": {"words_drawn": st["work"][5], "words_drawn_by_warmup": st["work"][6],
+                    "mt_twists": st["work"][7], "mt_fallback_samples": st["mt_fallbacks"]},
+        "algorithmic": "the reference's operators for the work done (uecraytracing_amd/flops.py lane_ops): "
+                       "FP64 flops + per sample the 397-step seeding walk (4 ops/step) + per engine word "
+                       "21 integer ops (next seeding step, twisted word, tempering) and 3 FP64 (canonical) "
+                       "+ the full engine's seeding and twists past draw 227",
+        "reconcile": pmc_lane_ops(),
+    }
     issue = None
     if facts and "valu_pipe_util" in facts and "valu_lane_utilization" in facts:
         issue = {"valu_busy": round(facts["valu_pipe_util"], 4),
@@ -436,14 +479,20 @@ def main():
             "hbm": {"algorithmic_bytes_per_launch": round(hbm_step / launches),
                     "achieved": round(hbm_gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(hbm_gbps / HBM_PEAK_GBPS, 7), "traffic": traffic,
-                    "traffic_over_algorithmic": round(traffic / (hbm_step / launches), 1) if traffic else None,
+                    "traffic_per_sample": round(traffic_ps, 3) if traffic_ps else None,
+                    "algorithmic_bytes_per_sample": round(alg_ps, 4),
+                    "traffic_over_algorithmic": round(traffic_ps / alg_ps, 1) if traffic_ps else None,
                     "device_bytes": tst["device_bytes"], "call_bytes": tst["call_bytes"],
                     "algorithmic": f"SURVEY §8(d): the RGB8 image ({pix_mine * 3} B) once per "
                                    f"step + the scene ({scene_bytes} B) once per workgroup "
                                    f"({tst['grid_blocks']} per launch); traffic = PMC FETCH_SIZE x2 + "
                                    f"WRITE_SIZE per launch (scratch: the start records, the colour "
                                    f"records, the processing order, MT fallback state)"},
-            "checks": {"launches_x_launch_ms_le_step": bool(launches * launch_ms <= ms_per_step * 1.001)},
+            # the union of the step's render spans can exceed the step (a step's first renders are
+            # enqueued while the previous step's still run): then launch_ms is the step / launches
+            "launch_ms_unclamped": round(busy_ms / launches, 4),
+            "launch_ms_clamped_to_step": bool(clamped),
+            "valu_ops": valu_ops,
             # render = the launches' spans summed (they overlap); render_busy = their union
             "step_breakdown_ms": {"render_spans_summed": round(tst["kernel_ms"], 3),
                                   "render_busy": round(busy_ms, 3),

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define YKGPU_ABI_VERSION 10u
+#define YKGPU_ABI_VERSION 11u
 
 /* Material kinds.  LAMBERTIAN / METAL(fuzz == 0) are the reference's (material.hpp:37-69);
  * METAL with fuzz > 0 (reflected + fuzz * the reference's random_in_unit_sphere,
@@ -184,19 +184,27 @@ typedef struct yk_render_stats {
   uint32_t grid_blocks;    /* persistent grid size                                     */
   double render_busy_ms;   /* union of the path-tracing launches' spans (wall time with at
                               least one launch running)                                 */
-  uint64_t work[8];        /* flag COUNT_WORK, FP64 (the FP64 flop model):
-                              [0] leaf tests with disc >= 0 (root bounds computed), hits
-                              shaded as [1] lambertian, [2] metal, [3] of them fuzzy,
-                              [4] dielectric; [5..7] 0                                   */
+  uint64_t work[8];        /* flag COUNT_WORK (the flop and lane-op models):
+                              FP64 only: [0] leaf tests with disc >= 0 (root bounds
+                              computed), hits shaded as [1] lambertian, [2] metal, [3] of
+                              them fuzzy, [4] dielectric; both precisions: [5] engine words
+                              drawn by all samples, [6] of them by the seed-walk kernel
+                              (the start's jitter and lens draws), [7] 624-word twists of
+                              the full mt19937 state (samples past 227 words)            */
   uint64_t device_bytes;   /* device memory the context holds after the call: scene, BVHs,
                               processing order, start-record (xor128: colour) ring, running
                               sums, MT and attenuation scratch, output buffers.
                               Buffers follow the calls: grown when a call needs more, given
                               back when it needs less than half                            */
   uint64_t call_bytes;     /* device memory THIS call needed (the same items sized to it):
-                              1920x1080x512 FP64 ~13.7 GB; a 270-row tile of 3840 ~7.4 GB   */
+                              1920x1080x512 FP64 ~18.1 GB; the 8-GPU split's tile of 3840x2160x1024
+                              (480 columns) ~9.8 GB; 1920x1080x4096 (config 5) ~69 GB       */
   double sclk_mhz;         /* the shader clock the render launches ran at: s_memtime over
                               s_memrealtime (100 MHz) of one wave per launch, averaged      */
+  uint32_t launch_spp;     /* samples per pixel of the call's largest launch (ABI 11)        */
+  uint32_t mem_shrinks;    /* times the launch size was halved because the device could not
+                              hold the rings (free memory short: slower, not an error; at
+                              launches of 2^24 sample slots the call fails with NOMEM)      */
 } yk_render_stats;
 
 typedef struct ykgpu_context ykgpu_context;
@@ -221,11 +229,16 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
 int ykgpu_render(ykgpu_context* ctx, const yk_render_params* params, uint8_t* rgb_host);
 
 /* Same, into device memory (row_count * Wt * 3 bytes on ctx's device), ordered on `stream`
- * (a hipStream_t; NULL = the context's own stream): the render starts after the work already
- * queued on `stream` and the image is complete for the work queued after it.  Internally the
- * kernels run on the context's own streams (render launches at the device's top stream
- * priority, the seed walks and the reduces below it) joined to `stream` by events.  Does not
- * synchronise. */
+ * (a hipStream_t; NULL = the context's own stream): the writes to rgb_device come after the work
+ * already queued on `stream`, and the image is complete for the work queued on `stream` after
+ * the call.  Internally the kernels run on the context's own streams (render launches at the
+ * device's top stream priority, the seed walks and the reduces below it) joined to `stream` by
+ * events.  A call enqueued while this context's previous call still runs, with the same ring
+ * geometry, overlaps it: its seed walks and renders start without waiting for `stream` (they
+ * read only the scene and the context's own buffers) and only its last reduce, which writes
+ * rgb_device, waits for `stream`.  YKGPU_OVERLAP=0 in the environment restores full ordering
+ * (every kernel of the call after the work queued on `stream` and after the whole previous
+ * call).  Does not synchronise. */
 int ykgpu_render_async(ykgpu_context* ctx, const yk_render_params* params, void* rgb_device,
                        void* stream);
 

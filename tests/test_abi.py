@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     lib = yk.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 10
+    assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 11
 
 
 def test_reference_camera_matches_camera_hpp():
@@ -115,12 +115,13 @@ def test_render_params_layout_matches_the_header():
 
 
 def test_render_stats_layout_matches_the_header():
-    """yk_render_stats ends with device_bytes at offset 312, call_bytes at 320 and sclk_mhz at 328
-    (include/ykgpu.h, ABI 10)."""
+    """yk_render_stats ends with device_bytes at offset 312, call_bytes at 320, sclk_mhz at 328 and
+    (ABI 11) launch_spp, mem_shrinks at 336, 340 (include/ykgpu.h)."""
     assert records.RenderStats.device_bytes.offset == 312
     assert records.RenderStats.call_bytes.offset == 320
     assert records.RenderStats.sclk_mhz.offset == 328
-    assert ctypes.sizeof(records.RenderStats) == 336
+    assert (records.RenderStats.launch_spp.offset, records.RenderStats.mem_shrinks.offset) == (336, 340)
+    assert ctypes.sizeof(records.RenderStats) == 344
 
 
 def test_invalid_arguments_are_reported():

@@ -152,3 +152,17 @@ def test_column_tiles_render_the_image_columns():
     p.col_stride = 1  # col_count == 0 (every column) with a stride set
     with pytest.raises(RuntimeError):
         oracle_lib.render(sc, cam, p)
+
+
+def test_rank_tile_refuses_an_empty_tile():
+    """with fewer than 8 x world columns (8-column bands) a rank would get an empty
+    column set, which the C-ABI reads as 'every column' (col_count 0) and rejects; rank_tile says
+    so up front, naming the row dealing, which still works for such an image."""
+    from uecraytracing_amd.tiles import rank_tile
+    with pytest.raises(ValueError, match="deal rows"):
+        rank_tile(7, 8, 40, 56, "cols")
+    assert rank_tile(6, 8, 40, 56, "cols")["cols"] == (48, 8, 8, 3)
+    assert rank_tile(7, 8, 40, 56, "rows")["rows"] == (7, 5, 8, 0)
+    with pytest.raises(ValueError, match="rank 5 would get none"):
+        rank_tile(5, 8, 5, 1920, "rows")
+    assert rank_tile(0, 1, 9, 4, "cols") == {"rows": (0, 9, 1, 0), "cols": None}

@@ -8,7 +8,9 @@ export TMPDIR=/tmp
 T=${1:-prof}
 mkdir -p gpurun_out/$T
 bash tools/pmc_profile.sh gpurun_out/$T/pmc || { echo PMC_FAILED; exit 3; }
-python3 tools/pmc_summary.py gpurun_out/$T/pmc "yk_render_persistent<true, 0>" final42_1920x1080x512_d50_n1 gpurun_out/$T/pmc_summary.json > /dev/null || exit 4
+# (pmc_profile.sh runs bench.py --steps 1 --warmup 1 per pass: two 1920x1080x512 calls)
+python3 tools/pmc_summary.py gpurun_out/$T/pmc "yk_render_persistent<true, 0>" final42_1920x1080x512_d50_n1 gpurun_out/$T/pmc_summary.json 2123366400 > /dev/null || exit 4
+python3 tools/pmc_summary.py gpurun_out/$T/pmc "yk_mt_warmup" final42_1920x1080x512_d50_n1 gpurun_out/$T/pmc_summary_warmup.json > /dev/null || exit 4
 cp gpurun_out/$T/pmc_summary.json profiles/pmc_summary.json
 timeout -k 10 400 python bench.py > gpurun_out/$T/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/$T/bench.log; exit 1; }
 grep '^{' gpurun_out/$T/bench.log | tail -1 > gpurun_out/$T/bench.json

@@ -19,6 +19,7 @@ def funcs(path):
                 cur = None
                 continue
             line = re.sub(r"\.LBB\d+_\d+", "L", line)
+            line = re.sub(r"\s*;.*$", "", line)  # trailing comments (basic-block numbers)
             if line.strip().startswith(";"):
                 continue
             out[cur].append(line)

@@ -2,6 +2,7 @@
 metrics (gfx950 corrections per MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half of a wide
 stream; GRBM_GUI_ACTIVE sums the 8 XCDs; SQ_* cycle counters are quad-cycles).
 usage: python tools/pmc_summary.py <pmc dir> [kernel-substring[|substring...]] [workload-tag] [out.json]
+                                  [samples rendered by the profiled dispatches]
 Several '|'-separated substrings (kernels that share a launch) sum their counters; "per dispatch"
 then means per dispatch of the LAST one (one per launch).
 VALU busy / lane utilisation / the wait fractions come from the summed counters too."""
@@ -44,6 +45,12 @@ if "SQ_WAVE_CYCLES" in per:
             out[k + "_frac"] = per[k] / per["SQ_WAVE_CYCLES"]
 if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     out["hbm_bytes_per_launch"] = per["FETCH_SIZE"] * 1024 * 2 + per["WRITE_SIZE"] * 1024
+    if len(sys.argv) > 5:
+        # per sample: the FETCH_SIZE pass's and the WRITE_SIZE pass's dispatches each render the
+        # given samples (one bench run per pass)
+        tot = (agg["FETCH_SIZE"] * 1024 * 2 + agg["WRITE_SIZE"] * 1024)
+        out["samples_per_pass"] = int(float(sys.argv[5]))
+        out["hbm_bytes_per_sample"] = tot / out["samples_per_pass"]
 if "SQ_INSTS_VALU" in per and "GRBM_GUI_ACTIVE" in per:
     # SIMD-32: a wave64 VALU instruction holds its SIMD 2 cycles (MI355X_MICROARCH.md)
     out["valu_pipe_util"] = per["SQ_INSTS_VALU"] * 2 / (1024 * per["GRBM_GUI_ACTIVE"] / 8)

@@ -82,6 +82,31 @@ struct XorShrU32 {  // x ^ (x >> 30): the seeding step's shift-xor
     asm volatile("v_lshrrev_b32 %1, 30, %0\n\tv_xor_b32 %0, %0, %1" : "+v"(x), "=&v"(t));
   }
 };
+// round 5 (the lane-op roofline's per-class issue costs, uecraytracing_amd/flops.py): one plain
+// 32-bit op, gfx950's three-input bitwise op, the u32 -> f64 conversion of every engine word, and
+// the seed walk's whole step as the kernel issues it (v_lshrrev + v_xor + v_mad_u64_u32)
+struct XorB32 {
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T) { asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x) : "v"(a)); }
+};
+struct Bitop3B32 {
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T b) { asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x78" : "+v"(x) : "v"(a), "v"(b)); }
+};
+struct CvtF64U32 {
+  using T = double;
+  static __device__ void op(T& x, T, T) { asm volatile("v_cvt_f64_u32 %0, 7" : "=v"(x)); }
+};
+struct WalkStep {
+  using T = uint32_t;
+  static __device__ void op(T& x, T a, T) {
+    uint32_t t;
+    uint64_t r, cc;
+    asm volatile("v_lshrrev_b32 %0, 30, %1\n\tv_xor_b32 %0, %1, %0" : "=&v"(t) : "v"(x));
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 7" : "=v"(r), "=s"(cc) : "v"(t), "v"(a));
+    x = (uint32_t)r;
+  }
+};
 struct CmpLtF64 {  // v_cmp into an SGPR pair, then used by a cndmask so it is not dead
   using T = uint32_t;
   static __device__ void op(T& x, T a, T b) {
@@ -312,6 +337,10 @@ int main(int argc, char** argv) {
     chip_rate<MulLoU32>("mul_lo_u32", 0, 1812433253u, 0, 7u, wps);
     chip_rate<MadU64U32>("mad_u64_u32", 0, 1812433253u, 0, 7u, wps);
     chip_rate<XorShrU32>("xor_shr_u32", 0, 0, 0, 7u, wps);
+    chip_rate<XorB32>("xor_b32", 0, 0x5bd1e995u, 0, 7u, wps);
+    chip_rate<Bitop3B32>("bitop3_b32", 0, 0x5bd1e995u, 0x9908b0dfu, 7u, wps);
+    chip_rate<CvtF64U32>("cvt_f64_u32", 0, 0, 0, 1.0, wps);
+    chip_rate<WalkStep>("walk_step", 0, 1812433253u, 0, 7u, wps);
   }
   for (int waves : {p.multiProcessorCount * 4, p.multiProcessorCount * 8, p.multiProcessorCount * 16}) {
     run<FmaF32>("fma_f32", 1.0000001f, 0.5f, 1.0f, waves);

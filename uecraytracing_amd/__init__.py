@@ -31,7 +31,7 @@ EXPORTS = (
     "ykgpu_group_create", "ykgpu_group_destroy", "ykgpu_group_size", "ykgpu_group_set_scene",
     "ykgpu_group_render", "ykgpu_group_get_stats", "ykgpu_render_devices",
 )
-ABI_VERSION = 10
+ABI_VERSION = 11
 SCENE_DIR = os.path.join(PKG_DIR, "scenes")  # committed scene files of the BASELINE configs
 
 _lib = None

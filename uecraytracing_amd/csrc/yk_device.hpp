@@ -206,6 +206,11 @@ struct MtLane {
 };
 // A sample used the scratch engine iff it drew more than 227 words.
 __device__ __forceinline__ bool mt_used_fallback(const MtLane& g) { return g.j > kLazyDraws; }
+// Work counters (YK_FLAG_COUNT_WORK; the VALU lane-op roofline, uecraytracing_amd/flops.py): the
+// words a sample's engine has drawn, and the scratch engine's 624-word twists they needed — the
+// first at draw 227 (mt_slow), then one per 624 draws (random.hpp:95-105, 114-131).
+__device__ __forceinline__ uint32_t rng_words(const MtLane& g) { return g.j; }
+__device__ __forceinline__ uint32_t rng_twists(const MtLane& g) { return g.j > kLazyDraws ? 1u + (g.j - 1u) / kMtN : 0u; }
 
 __device__ __forceinline__ void mt_start(MtLane& g, uint32_t seed) {
   g.seed = seed;
@@ -334,12 +339,14 @@ __device__ __forceinline__ uint32_t sample_seed(uint32_t mode, uint64_t key, uin
 // (:19-32); four words of state, so a sample needs neither the x_397 warm-up nor scratch.
 struct X128Lane {
   uint32_t x, y, z, w;
+  uint32_t n;  // words drawn (work counters only: dead in the production instances)
 };
 __device__ __forceinline__ void x128_start(X128Lane& g, uint32_t seed) {
   g.x = 123456789u;
   g.y = 362436069u;
   g.z = 521288629u;
   g.w = 88675123u ^ seed;
+  g.n = 0;
 }
 __device__ __forceinline__ uint32_t x128_next(X128Lane& g) {  // operator(), :34-40
   const uint32_t t = g.x ^ (g.x << 11);
@@ -347,9 +354,12 @@ __device__ __forceinline__ uint32_t x128_next(X128Lane& g) {  // operator(), :34
   g.y = g.z;
   g.z = g.w;
   g.w = (g.w ^ (g.w >> 19)) ^ (t ^ (t >> 8));
+  ++g.n;
   return g.w;
 }
 __device__ __forceinline__ bool mt_used_fallback(const X128Lane&) { return false; }
+__device__ __forceinline__ uint32_t rng_words(const X128Lane& g) { return g.n; }
+__device__ __forceinline__ uint32_t rng_twists(const X128Lane&) { return 0u; }
 
 __device__ __forceinline__ bool rng_lazy_ok(const X128Lane&, uint32_t) { return true; }
 

@@ -111,8 +111,9 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #endif
 // the visit's slab constants as one op_sel-read register pair per axis and bound (yk_slab.hpp):
 // FP64 123 -> 115 VGPRs and no faster (512 spp 173.9 -> 174.2 ms: the FP64 kernel keeps the
-// broadcast pairs); FP32 125 -> 111 VGPRs and faster (195.3 -> 190.1 ms, profiles/r04_ab/f32/);
-// yk_render_dual (which needs the registers) uses them always.  YK_SLAB_PAIRS sets both (A/B).
+// broadcast pairs); FP32 125 -> 111 VGPRs and faster (195.3 -> 190.1 ms, profiles/r04_ab/f32/).
+// YK_SLAB_PAIRS sets both (A/B).  (Round 4's two-paths-per-lane kernel, which lost its A/B, is
+// kept as a patch beside its evidence: profiles/r04_ab/dual/yk_dual.patch.)
 #ifdef YK_SLAB_PAIRS
 #define YK_SLAB_PAIRS_F64 YK_SLAB_PAIRS
 #define YK_SLAB_PAIRS_F32 YK_SLAB_PAIRS
@@ -585,7 +586,7 @@ __device__ __forceinline__ void rng_init(ykd::MtLane& g, const KernelArgs& ka, u
   g.state = ka.mt_scratch + (size_t)gid * ykd::kMtN;
   g.a0 = g.a1 = g.b = g.j = g.seed = 0;
 }
-__device__ __forceinline__ void rng_init(ykd::X128Lane& g, const KernelArgs&, uint32_t) { g.x = g.y = g.z = g.w = 0; }
+__device__ __forceinline__ void rng_init(ykd::X128Lane& g, const KernelArgs&, uint32_t) { g.x = g.y = g.z = g.w = g.n = 0; }
 
 // A sample's engine from its seed alone (xor128, and an mt19937 start no StartRec serves):
 // mt19937 walks its 397 seeding steps here
@@ -695,6 +696,8 @@ void yk_render_persistent(KernelArgs ka) {
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_node = 0, n_lin = 0, n_ncall = 0, n_nit = 0;
   uint32_t n_dpos = 0;  // leaf tests with disc >= 0 (their root bounds are computed)
   uint32_t n_lamb = 0, n_metal = 0, n_fuzz = 0, n_diel = 0;  // hits shaded per material kind
+  // engine words drawn (the warm-up's start words among them) and scratch-engine twists
+  uint32_t n_words = 0, n_swords = 0, n_twist = 0;
 
   YK_STAMPS_BEGIN(ka.counters, lane);
   uint32_t slot = 0, depth = 0, nstk = 0;
@@ -755,6 +758,7 @@ void yk_render_persistent(KernelArgs ka) {
         __builtin_memcpy((char*)&r + 48, &rq3, 16);
         pre = r.j != kNoStart;
         if (pre) {
+          if (kCount) n_swords += r.j;
           g.seed = seed;  // (the scratch engine's seeding needs it)
           g.a0 = r.a0;
           g.a1 = r.a1;
@@ -1176,6 +1180,7 @@ void yk_render_persistent(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
+      if (kCount) n_words += ykd::rng_words(g), n_twist += ykd::rng_twists(g);
       // the sample's colour; yk_reduce_samples adds them in sample order
       colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
@@ -1198,6 +1203,9 @@ void yk_render_persistent(KernelArgs ka) {
     atomicAdd(&ka.counters[26], (unsigned long long)n_metal);
     atomicAdd(&ka.counters[27], (unsigned long long)n_fuzz);
     atomicAdd(&ka.counters[28], (unsigned long long)n_diel);
+    atomicAdd(&ka.counters[29], (unsigned long long)n_words);
+    atomicAdd(&ka.counters[30], (unsigned long long)n_swords);
+    atomicAdd(&ka.counters[31], (unsigned long long)n_twist);
   }
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
@@ -1214,7 +1222,6 @@ RenderKernel fp64_kernel(bool lds, int mode) {
   return k[(lds ? 8 : 0) + (mode & 7)];
 }
 
-#include "yk_dual.hpp"
 #endif  // YK_SPLIT != 2
 
 #if YK_SPLIT != 1
@@ -1349,6 +1356,7 @@ void yk_render_f32(KernelArgs ka) {
   rng_init(g, ka, gid);
   uint16_t* const id_spill = ka.id_scratch + (size_t)gid * ka.id_stride;
   uint32_t n_seg = 0, n_test = 0, n_sqrt = 0, n_fb = 0, n_nit = 0, n_ncall = 0, n_node = 0, n_lin = 0;
+  uint32_t n_words = 0, n_swords = 0, n_twist = 0;  // as in yk_render_persistent
   YK_STAMPS_BEGIN(ka.counters, lane);
   const float tmin = (float)ka.t_min;  // world.hit(r, 0.001, ...) converts to T (hittable.hpp:32)
   uint32_t slot = 0, depth = 0, nstk = 0;
@@ -1398,6 +1406,7 @@ void yk_render_f32(KernelArgs ka) {
         __builtin_memcpy((char*)&r + 32, &rq2, 16);
         pre = r.j != kNoStart;
         if (pre) {
+          if (kCount) n_swords += r.j;
           g.seed = seed;
           g.a0 = r.a0;
           g.a1 = r.a1;
@@ -1788,6 +1797,7 @@ void yk_render_f32(KernelArgs ka) {
         L_b = m.ab * L_b;
       }
       if (ykd::mt_used_fallback(g)) ++n_fb;
+      if (kCount) n_words += ykd::rng_words(g), n_twist += ykd::rng_twists(g);
       colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
@@ -1803,6 +1813,9 @@ void yk_render_f32(KernelArgs ka) {
     atomicAdd(&ka.counters[5], (unsigned long long)n_lin);
     atomicAdd(&ka.counters[6], (unsigned long long)n_ncall);
     atomicAdd(&ka.counters[7], (unsigned long long)n_nit);
+    atomicAdd(&ka.counters[29], (unsigned long long)n_words);
+    atomicAdd(&ka.counters[30], (unsigned long long)n_swords);
+    atomicAdd(&ka.counters[31], (unsigned long long)n_twist);
   }
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
 }
@@ -1852,14 +1865,13 @@ struct DevTree {
   double origin_bound = 0;  // |o|_inf beyond which a ray takes the linear scan (< 0: every ray)
   uint32_t geo_off = 0, ids_off = 0;  // leaf geometry and ids in LDS, after the nodes
   size_t bytes = 0;                   // device bytes of nodes, leaf geometry and ids
-  // LDS plan per kernel shape: [0] kBlock threads (mt19937 instances), [1] kBlockX128 (xor128),
-  // [2] kDualBlock threads with two paths each (yk_render_dual)
+  // LDS plan per kernel shape: [0] kBlock threads (mt19937 instances), [1] kBlockX128 (xor128)
   struct Plan {
     bool in_lds = false;
     uint32_t lds_bytes = 0, stack_off = 0, stack_cap = 0, stack_entries = 0;
     uint32_t tgeo_off = 0, mat_off = 0;  // shading tables in LDS (FP64 kernel), 0: none
     int grid = 0;                        // persistent blocks: occupancy x CUs
-  } plan[3];
+  } plan[2];
   void release() {
     (void)hipFree(nodes);
     (void)hipFree(leaf_geo);
@@ -1895,8 +1907,18 @@ struct ykgpu_context {
   // a global launch counter that numbers the ring slots, the scratch parity and the render
   // stream across calls
   std::vector<hipEvent_t> lev_prev;
-  uint32_t prev_n = 0, prev_R = 0, prev_CR = 0;
-  uint64_t prev_geom = 0;   // hash of (slots per launch buffer, record size, ring buffers)
+  uint32_t prev_n = 0;
+  // the previous call's ring and scratch geometry: a call overlaps it only when every field is
+  // equal (launch() `ov`; equal slot offsets in every ring buffer and scratch slice)
+  struct RingGeom {
+    uint64_t nps = 0, K = 0, welem = 0, warm_ring = 0, col_ring = 0, lanes = 0, id_stride = 0;
+    const void *warm = nullptr, *col = nullptr, *mt = nullptr, *ids = nullptr;
+    bool operator==(const RingGeom& o) const {
+      return nps == o.nps && K == o.K && welem == o.welem && warm_ring == o.warm_ring && col_ring == o.col_ring &&
+             lanes == o.lanes && id_stride == o.id_stride && warm == o.warm && col == o.col && mt == o.mt &&
+             ids == o.ids;
+    }
+  } prev_geom;
   uint64_t prev_shape = 0;  // (nps, kmax, precision, engine) of the previous call: launch() `inflight`
   bool prev_ok = false;
   bool prev_enqueued = false;  // the previous call's launches were all enqueued (its events exist)
@@ -1937,6 +1959,17 @@ struct ykgpu_group {
 };
 
 namespace {
+
+// A/B knobs: environment overrides of the launch schedule, rings, grids and tree build that the
+// A/B tools time (tools/abtime.py `lib@YKGPU_X=v`).  They exist only in variant builds
+// (tools/build_def_variant.sh <name> -DYK_AB_KNOBS): in the product library ab_knob() is a
+// constant nullptr, so nothing in a caller's environment changes the schedule or the tree.  The
+// documented diagnostics YKGPU_TIMELINE and YKGPU_OVERLAP stay.
+#ifdef YK_AB_KNOBS
+const char* ab_knob(const char* name) { return std::getenv(name); }
+#else
+constexpr const char* ab_knob(const char*) { return nullptr; }
+#endif
 
 uint64_t host_row_y(const yk_render_params* p, uint32_t t) {
   const uint32_t L = p->row_band_log2;
@@ -2054,6 +2087,10 @@ constexpr uint32_t kLaunchesPerCall = YK_LAUNCHES_PER_CALL;
 #define YK_LAUNCH_SLOTS (1u << 25)
 #endif
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
+// Under memory pressure (launch()): launches shrink down to this many sample slots before a call
+// fails with YK_ERR_NOMEM, and the rings leave kMemReserve of the device free
+constexpr uint64_t kMemFloorSlots = 1ull << 24;
+constexpr size_t kMemReserve = (size_t)512 << 20;
 // Start-record ring: the warm-ups run on ctx->aux, beside the render launches (their wave slots
 // and VGPRs fit next to the render kernel's, and the render leaves most VALU issue slots idle),
 // into a ring of min(launches, kWarmRingDepth) launch buffers (YKGPU_WARM_RING overrides); warm-up
@@ -2101,7 +2138,7 @@ constexpr uint32_t kTile = YK_TILE;  // processing blocks of kTile x kTile pixel
 // cost 17% more per sample, measured).
 int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride) {
   // (A/B knob: YKGPU_ORDER=1 takes the block rows bottom-up)
-  const char* oe = std::getenv("YKGPU_ORDER");
+  const char* oe = ab_knob("YKGPU_ORDER");
   const uint32_t mode = oe ? (uint32_t)std::atoi(oe) : 0u;
   if (ctx->d_order && ctx->order_w == W && ctx->order_rows == rows && ctx->order_stride == stride &&
       ctx->order_mode == mode)
@@ -2142,7 +2179,7 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride)
 // before the next launch's workgroups (one per CU, 768 threads and most of the LDS) fit.
 hipError_t create_render_stream(hipStream_t* s) {
   int least = 0, greatest = 0;
-  const char* e = std::getenv("YKGPU_RENDER_PRIO");
+  const char* e = ab_knob("YKGPU_RENDER_PRIO");
   if ((e && std::atoi(e) == 0) || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
   return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
@@ -2158,7 +2195,7 @@ hipError_t create_render_stream(hipStream_t* s) {
 #endif
 uint32_t col_ring() {
   uint32_t r = YK_COL_RING;
-  if (const char* e = std::getenv("YKGPU_COL_RING")) r = (uint32_t)std::max(2, std::min(8, std::atoi(e)));
+  if (const char* e = ab_knob("YKGPU_COL_RING")) r = (uint32_t)std::max(2, std::min(8, std::atoi(e)));
   return r;
 }
 
@@ -2166,7 +2203,7 @@ uint32_t col_ring() {
 // 0 = one thread per slot), so a reduce never floods the CUs a render launch is about to take
 uint32_t reduce_blocks(const ykgpu_context* ctx, uint32_t nps) {
   uint32_t cap = (uint32_t)ctx->cus * 4;
-  if (const char* e = std::getenv("YKGPU_RED_BLOCKS")) cap = (uint32_t)std::max(0, std::atoi(e));
+  if (const char* e = ab_knob("YKGPU_RED_BLOCKS")) cap = (uint32_t)std::max(0, std::atoi(e));
   const uint32_t full = (nps + 255) / 256;
   return cap ? std::max(1u, std::min(full, cap)) : full;
 }
@@ -2178,18 +2215,8 @@ uint32_t reduce_blocks(const ykgpu_context* ctx, uint32_t nps) {
 // with (512-spp FP32 A/B: 32 -> 205.2 ms, 4 -> 202.4, 3 -> 202.4, 2 -> 201.3)
 uint32_t warm_per_cu(bool f32) {
   uint32_t per_cu = f32 ? 2u : 32u;
-  if (const char* e = std::getenv("YKGPU_WARM_PER_CU")) per_cu = (uint32_t)std::max(1, std::atoi(e));
+  if (const char* e = ab_knob("YKGPU_WARM_PER_CU")) per_cu = (uint32_t)std::max(1, std::atoi(e));
   return per_cu;
-}
-
-// yk_render_dual (two paths per lane) for the FP64 mt19937 renders when YKGPU_DUAL=1 (A/B; the
-// production path is the one-path yk_render_persistent: DESIGN.md §8, round 4)
-#ifndef YK_DUAL
-#define YK_DUAL 0
-#endif
-bool dual_enabled() {
-  const char* e = std::getenv("YKGPU_DUAL");
-  return e ? std::atoi(e) != 0 : YK_DUAL != 0;
 }
 
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
@@ -2197,13 +2224,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const bool f32 = p->precision == YK_PRECISION_FP32;
   const bool x128 = p->rng == YK_RNG_XOR128;  // no warm-ups, no MT scratch
   const DevTree& tree = f32 ? ctx->t32 : ctx->t64;
-  // FP64 mt19937 with YKGPU_DUAL=1 (A/B): two paths per lane (yk_render_dual), except for the
-  // one-lane diagnostic (the single-path counting instance's)
-  const bool dual = !f32 && !x128 && !(p->flags & YK_FLAG_ONE_LANE) && dual_enabled();
-  const DevTree::Plan& plan = tree.plan[dual ? 2 : (x128 ? 1 : 0)];
-  const int grid = plan.grid, block = dual ? kDualBlock : block_of(x128);
-  const int paths = dual ? 2 : 1;  // paths per lane: MT and attenuation scratch per path
-  int rc = ensure_scratch(ctx, p->max_depth, (size_t)grid * block * paths, !x128);
+  const DevTree::Plan& plan = tree.plan[x128 ? 1 : 0];
+  const int grid = plan.grid, block = block_of(x128);
+  int rc = ensure_scratch(ctx, p->max_depth, (size_t)grid * block, !x128);
   if (rc) return rc;
   // YK_SEED_RANDOM_DEVICE without a key: one from std::random_device per call (source.cpp:159)
   uint64_t seed_key = 0;
@@ -2237,7 +2260,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // a drain.  Neither floor nor cap exceeds the colour budget or 2^31 slots.
   const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
   uint64_t launch_slots = kLaunchSlots;  // (A/B knob: YKGPU_LAUNCH_SLOTS)
-  if (const char* e = std::getenv("YKGPU_LAUNCH_SLOTS")) launch_slots = (uint64_t)std::max(1ll, std::atoll(e));
+  if (const char* e = ab_knob("YKGPU_LAUNCH_SLOTS")) launch_slots = (uint64_t)std::max(1ll, std::atoll(e));
   const uint64_t slot_spp = (launch_slots + nps - 1) / nps;
   // A long call takes longer launches: every launch pays a drain whose length is the longest path
   // of its last samples, and many launches per call buy nothing once there are ~32 (config 5,
@@ -2246,45 +2269,21 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // costs 5%; profiles/r04_ab/launch_size/).  The rings grow with the launch: config 5 holds
   // ~64 GB (3 x 2.07M x 121 x 64 B of start records, 2 x 2.07M x 121 x 32 B of colours).
   uint64_t launch_spp = std::max<uint64_t>(kLaunchSpp, spp / kLaunchesPerCall);
-  if (const char* e = std::getenv("YKGPU_LAUNCH_SPP")) launch_spp = (uint64_t)std::max(1, std::atoi(e));  // (A/B)
-  const uint32_t kmax = (uint32_t)std::max<uint64_t>(
+  if (const char* e = ab_knob("YKGPU_LAUNCH_SPP")) launch_spp = (uint64_t)std::max(1, std::atoi(e));  // (A/B)
+  const uint32_t kideal = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
                              std::max<uint64_t>({launch_spp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
-  std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
-  // A call enqueued while the previous one still runs (back-to-back steps) starts its first
-  // warm-ups under the previous call's last launches, so it needs no small first launch: every
-  // launch at kmax — the frame is 16 launches of 32 (bench 8 steps: 172.4 ms per step with 4, 8,
-  // 16, 32; 170.8 with 8, 32; 168.4 with 32, 32, ...; profiles/r04_ab/schedule/), the 8-way tile
-  // of config 3 four of ~130 (23.1 ms per call starting at 32, 21.8 at 128; the 4-way tile 44.3
-  // -> 43.0 ms starting at 64; profiles/r04_ab/tiles/)
-  // (A/B knobs: YKGPU_FIRST_LAUNCH, YKGPU_SCHED_GROW and their _OV forms — the first launch's
-  // samples per pixel and the factor each next launch grows by until kmax)
-  // (only for a call of the previous one's shape, whose rings it can overlap: launch() `ov`)
-  const uint64_t shape = ((uint64_t)nps << 24) ^ ((uint64_t)kmax << 2) ^ (f32 ? 2u : 0u) ^ (x128 ? 1u : 0u);
-  bool inflight = false;
-  if (ctx->prev_enqueued && ctx->prev_ok && !ctx->dirty && ctx->prev_shape == shape && ctx->prev_n > 0 &&
-      ctx->lev.size() >= 6ull * ctx->prev_n)
-    inflight = hipEventQuery(ctx->lev[6 * (ctx->prev_n - 1) + 5]) == hipErrorNotReady;
-  uint32_t first_k = inflight ? (kFirstLaunchOv ? kFirstLaunchOv : kmax) : kFirstLaunch;
-  uint32_t grow_k = inflight ? kSchedGrowOv : kSchedGrow;
-  if (const char* e = std::getenv(inflight ? "YKGPU_FIRST_LAUNCH_OV" : "YKGPU_FIRST_LAUNCH"))
-    first_k = (uint32_t)std::max(1, std::atoi(e));
-  if (const char* e = std::getenv(inflight ? "YKGPU_SCHED_GROW_OV" : "YKGPU_SCHED_GROW"))
-    grow_k = (uint32_t)std::max(2, std::atoi(e));
-  for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
-    uint32_t take = std::min(k, spp - s0);
-    const uint32_t rest = spp - (s0 + take);
-    if (rest > 0 && rest < std::max(1u, take / 4)) {
-      // a short tail launch would cost its own ramp and drain: fold it in, or split the
-      // remainder into two equal launches when one would exceed the colour budget
-      take = spp - s0 <= kmax ? spp - s0 : (spp - s0 + 1) / 2;
-    }
-    sched.emplace_back(s0, take);
-    s0 += take;
-    k = std::min(grow_k * k, kmax);
-  }
-  uint32_t K = 0;  // largest launch
-  for (auto& l : sched) K = std::max(K, l.second);
+  // A device short of memory (other contexts, other processes) makes the call slower, not fatal:
+  // the rings are sized for launches of kmax samples per pixel, and when the device cannot hold
+  // them — free memory (hipMemGetInfo) plus what this context's rings already hold, or a
+  // hipMalloc that fails anyway — kmax halves, down to launches of kMemFloorSlots sample slots,
+  // before the call fails with YK_ERR_NOMEM (yk_render_stats.launch_spp / mem_shrinks report it).
+  const uint32_t kfloor = (uint32_t)std::min<uint64_t>(kideal, std::max<uint64_t>(1, (kMemFloorSlots + nps - 1) / nps));
+  uint32_t kmax = kideal, mem_shrinks = 0;
+  auto shrink = [&]() {
+    kmax = std::max(kfloor, kmax / 2);
+    ++mem_shrinks;
+  };
   // a buffer follows the call: grown when it is too small, and given back when the call needs
   // less than half of it (device_bytes then reports about what the call holds)
   auto grow = [&](auto*& ptr, size_t& cap, size_t need, size_t elem) -> int {
@@ -2297,22 +2296,83 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     cap = need;
     return YK_OK;
   };
-  const uint32_t nlaunch = (uint32_t)sched.size();
+  std::vector<std::pair<uint32_t, uint32_t>> sched;  // (s0, samples)
+  uint64_t shape = 0;
+  bool inflight = false;
+  uint32_t K = 0, nlaunch = 0, kWarmRing = 0, kColRing = 0;
   // start records (StartRec, FP32 StartRecF: each sample's whole start)
   const size_t welem = f32 ? sizeof(StartRecF) : sizeof(StartRec);
-  uint32_t kWarmRing = std::min(nlaunch, kWarmRingDepth);
-  if (const char* e = std::getenv("YKGPU_WARM_RING"))  // (A/B) launch buffers in the ring
-    kWarmRing = (uint32_t)std::min<uint64_t>(nlaunch, (uint64_t)std::max(2, std::atoi(e)));
   // (diagnostic, timing only) YKGPU_ABL_WARM_FIRST=1: every launch's warm-up runs, and finishes,
   // before the first render: render_busy_ms then times the render kernels without the seed walks
   // beside them (same images)
-  const bool warm_first = std::getenv("YKGPU_ABL_WARM_FIRST") != nullptr && !x128;
-  if (warm_first) kWarmRing = nlaunch;
-  // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
-  // reduce c (stream red) overlaps the renders after it
-  const uint32_t kColRing = std::min(nlaunch, col_ring());
-  if (!x128 && (rc = grow(ctx->d_warm, ctx->warm_cap, (size_t)kWarmRing * nps * K * welem, 1))) return rc;
-  if ((rc = grow(ctx->d_col, ctx->col_cap, (size_t)kColRing * nps * K * kColStride, sizeof(double)))) return rc;
+  const bool warm_first = ab_knob("YKGPU_ABL_WARM_FIRST") != nullptr && !x128;
+  for (;;) {
+    // A call enqueued while the previous one still runs (back-to-back steps) starts its first
+    // warm-ups under the previous call's last launches, so it needs no small first launch: every
+    // launch at kmax — the frame is 16 launches of 32 (bench 8 steps: 172.4 ms per step with 4, 8,
+    // 16, 32; 170.8 with 8, 32; 168.4 with 32, 32, ...; profiles/r04_ab/schedule/), the 8-way tile
+    // of config 3 four of ~130 (23.1 ms per call starting at 32, 21.8 at 128; the 4-way tile 44.3
+    // -> 43.0 ms starting at 64; profiles/r04_ab/tiles/)
+    // (A/B knobs: YKGPU_FIRST_LAUNCH, YKGPU_SCHED_GROW and their _OV forms — the first launch's
+    // samples per pixel and the factor each next launch grows by until kmax)
+    // (only for a call of the previous one's shape, whose rings it can overlap: launch() `ov`)
+    shape = ((uint64_t)nps << 24) ^ ((uint64_t)kmax << 2) ^ (f32 ? 2u : 0u) ^ (x128 ? 1u : 0u);
+    inflight = false;
+    if (ctx->prev_enqueued && ctx->prev_ok && !ctx->dirty && ctx->prev_shape == shape && ctx->prev_n > 0 &&
+        ctx->lev.size() >= 6ull * ctx->prev_n)
+      inflight = hipEventQuery(ctx->lev[6 * (ctx->prev_n - 1) + 5]) == hipErrorNotReady;
+    uint32_t first_k = inflight ? (kFirstLaunchOv ? kFirstLaunchOv : kmax) : kFirstLaunch;
+    uint32_t grow_k = inflight ? kSchedGrowOv : kSchedGrow;
+    if (const char* e = ab_knob(inflight ? "YKGPU_FIRST_LAUNCH_OV" : "YKGPU_FIRST_LAUNCH"))
+      first_k = (uint32_t)std::max(1, std::atoi(e));
+    if (const char* e = ab_knob(inflight ? "YKGPU_SCHED_GROW_OV" : "YKGPU_SCHED_GROW"))
+      grow_k = (uint32_t)std::max(2, std::atoi(e));
+    sched.clear();
+    for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
+      uint32_t take = std::min(k, spp - s0);
+      const uint32_t rest = spp - (s0 + take);
+      if (rest > 0 && rest < std::max(1u, take / 4)) {
+        // a short tail launch would cost its own ramp and drain: fold it in, or split the
+        // remainder into two equal launches when one would exceed the colour budget
+        take = spp - s0 <= kmax ? spp - s0 : (spp - s0 + 1) / 2;
+      }
+      sched.emplace_back(s0, take);
+      s0 += take;
+      k = std::min(grow_k * k, kmax);
+    }
+    K = 0;  // largest launch
+    for (auto& l : sched) K = std::max(K, l.second);
+    nlaunch = (uint32_t)sched.size();
+    kWarmRing = std::min(nlaunch, kWarmRingDepth);
+    if (const char* e = ab_knob("YKGPU_WARM_RING"))  // (A/B) launch buffers in the ring
+      kWarmRing = (uint32_t)std::min<uint64_t>(nlaunch, (uint64_t)std::max(2, std::atoi(e)));
+    if (warm_first) kWarmRing = nlaunch;
+    // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
+    // reduce c (stream red) overlaps the renders after it
+    kColRing = std::min(nlaunch, col_ring());
+    const size_t need_warm = x128 ? 0 : (size_t)kWarmRing * nps * K * welem;
+    const size_t need_col = (size_t)kColRing * nps * K * kColStride * sizeof(double);
+    if (kmax > kfloor && (need_warm > ctx->warm_cap || need_col > ctx->col_cap * sizeof(double))) {
+      // the rings must grow: does the device have room for them?
+      size_t free_b = 0, total_b = 0;
+      if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+        const size_t held = ctx->warm_cap + ctx->col_cap * sizeof(double);
+        if (need_warm + need_col + kMemReserve > free_b + held) {
+          shrink();
+          continue;
+        }
+      }
+    }
+    rc = x128 ? YK_OK : grow(ctx->d_warm, ctx->warm_cap, need_warm, 1);
+    if (!rc) rc = grow(ctx->d_col, ctx->col_cap, (size_t)kColRing * nps * K * kColStride, sizeof(double));
+    if (rc == YK_ERR_NOMEM && kmax > kfloor) {
+      (void)hipGetLastError();  // (the failed hipMalloc's error must not surface at a later launch)
+      shrink();
+      continue;
+    }
+    if (rc) return rc;
+    break;
+  }
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
@@ -2432,11 +2492,24 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // YKGPU_OVERLAP=0 (A/B) keeps every call behind the caller's stream, as do xor128 calls (no
   // warm-up kernel to clear their slot counters) and any call after a failed one.
   const uint64_t g0 = ctx->g_next;
-  const uint64_t geom = ((uint64_t)nps * K * welem) ^ ((uint64_t)(uintptr_t)ctx->d_warm << 1) ^
-                        ((uint64_t)(uintptr_t)ctx->d_col << 2) ^ ((uint64_t)kWarmRing << 56) ^ ((uint64_t)kColRing << 60);
+  // (every field that places a launch's start records, colours or per-lane scratch: a call whose
+  // K, record size or lane count differs would address other offsets of the same buffers, and its
+  // ring waits would not cover the previous call's launches there)
+  ykgpu_context::RingGeom geom;
+  geom.nps = nps;
+  geom.K = K;
+  geom.welem = welem;
+  geom.warm_ring = kWarmRing;
+  geom.col_ring = kColRing;
+  geom.lanes = (uint64_t)grid * block;
+  geom.id_stride = ctx->id_stride;
+  geom.warm = ctx->d_warm;
+  geom.col = ctx->d_col;
+  geom.mt = ctx->d_mt;
+  geom.ids = ctx->d_ids;
   const char* ove = std::getenv("YKGPU_OVERLAP");
   const bool ov = !x128 && !warm_first && !(ove && std::atoi(ove) == 0) && ctx->prev_ok && ctx->prev_geom == geom &&
-                  ctx->prev_R == kWarmRing && ctx->prev_CR == kColRing && ctx->prev_n >= std::max(kWarmRing, kColRing);
+                  ctx->prev_n >= std::max(kWarmRing, kColRing);
   if (ctx->dirty && (rc = quiesce(ctx))) return rc;  // a failed call's work: wait it out on the host
   const bool after_prev = ctx->prev_enqueued && !ctx->dirty && !ov;
   ctx->prev_ok = false;  // (until this call has been enqueued)
@@ -2465,6 +2538,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ctx->lev.push_back(e);
   }
   ctx->lev_used = 6 * nlaunch;
+  // the caller's stream clears this call's slot counters (xor128) and work counters below: before
+  // that it waits for the previous call, whose renders may still use both (it may have been
+  // enqueued on another stream)
+  if (after_prev) YK_HIP(hipStreamWaitEvent(st, ctx->lev_prev[6 * (ctx->prev_n - 1) + 5], 0));
   if (x128) YK_HIP(hipMemsetAsync(ctx->d_counter, 0, nlaunch * sizeof(uint32_t), st));
   if (!ov) {
     YK_HIP(hipMemsetAsync(ctx->d_stats, 0, kCounters * sizeof(unsigned long long), st));
@@ -2530,7 +2607,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     // only on its own start records and colour buffer, so its blocks take the CUs that launch c's
     // draining blocks free (per-lane scratch, slot counter and colours are per launch parity)
     const hipStream_t rs = (g & 1) ? ctx->alt : ctx->ren;
-    const size_t lanes = (size_t)grid * block * paths;
+    const size_t lanes = (size_t)grid * block;
     ka.mt_scratch = ctx->d_mt ? ctx->d_mt + (g & 1) * lanes * ykd::kMtN : nullptr;
     ka.id_scratch = ctx->d_ids + (g & 1) * lanes * ctx->id_stride;
     YK_HIP(hipStreamWaitEvent(rs, ev[1], 0));  // its start records
@@ -2546,9 +2623,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     if (f32)
       hipLaunchKernelGGL(f32_kernel(plan.in_lds, (count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(block),
                          plan.lds_bytes, rs, ka);
-    else if (dual)
-      hipLaunchKernelGGL(dual_kernel(plan.in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0)),
-                         dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
     else
       hipLaunchKernelGGL(fp64_kernel(plan.in_lds, (count ? 1 : 0) | (ka.seed_mode == YK_SEED_RANDOM_DEVICE ? 2 : 0) |
                                                       (x128 ? 4 : 0)),
@@ -2573,8 +2647,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   YK_HIP(hipEventRecord(ctx->ev1, st));
   ctx->g_next = g0 + nlaunch;
   ctx->prev_n = nlaunch;
-  ctx->prev_R = kWarmRing;
-  ctx->prev_CR = kColRing;
   ctx->prev_geom = geom;
   ctx->prev_shape = shape;
   ctx->prev_ok = !x128 && !warm_first;
@@ -2584,10 +2656,12 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ctx->stats.samples = (uint64_t)p->row_count * tile_width(p) * p->samples_per_pixel;
   ctx->stats.launches = launches;
   ctx->stats.grid_blocks = (uint32_t)grid;
+  ctx->stats.launch_spp = K;
+  ctx->stats.mem_shrinks = mem_shrinks;
   ctx->stats.seed_key = seed_key;
   // what this call needed (device_bytes: what the context holds)
   {
-    const uint64_t lanes = (uint64_t)grid * block * paths;
+    const uint64_t lanes = (uint64_t)grid * block;
     uint64_t cb = ctx->t64.bytes + ctx->t32.bytes +
                   (uint64_t)ctx->nspheres * (sizeof(SphereGeo) + sizeof(SphereMat) + sizeof(float4));
     cb += (uint64_t)kColRing * nps * K * kColStride * sizeof(double) + (x128 ? 0 : (uint64_t)kWarmRing * nps * K * welem);
@@ -2689,7 +2763,7 @@ int finish_stats(ykgpu_context* ctx) {
 // (for the occupancy).
 int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
                 double cam_ext, const ykbvh::Options& opt, uint32_t leaf_cap, const void* geo, size_t elem,
-                size_t tgeo_elem, const RenderKernel (&kern)[3][2]) {
+                size_t tgeo_elem, const RenderKernel (&kern)[2][2]) {
   const uint32_t count = (uint32_t)radii.size();
   if (opt.max_leaf > leaf_cap) return fail(YK_ERR_UNSUPPORTED, "BVH leaf size above the kernel's leaf capacity");
   const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
@@ -2731,12 +2805,11 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
   const size_t mat_bytes = tgeo_elem ? a16(count * sizeof(SphereMat)) : 0;
   t.geo_off = (uint32_t)a16(t.n_nodes * sizeof(DevNode));
   t.ids_off = t.geo_off + (uint32_t)a16(count * elem);
-  for (int v = 0; v < 3; ++v) {
+  for (int v = 0; v < 2; ++v) {
     DevTree::Plan& pl = t.plan[v];
-    // threads per workgroup, and traversal stacks per workgroup (one per path: two per thread in
-    // yk_render_dual)
-    const int blk = v == 2 ? kDualBlock : block_of(v == 1);
-    const int rays = v == 2 ? kDualRays : blk;
+    // threads per workgroup = traversal stacks per workgroup
+    const int blk = block_of(v == 1);
+    const int rays = blk;
     // a CU holds one workgroup of >= 512 threads (768 / blk of smaller ones); 2 KB below the
     // share: the hardware's allocation granularity (3 blocks of 54144 bytes measured only 2
     // resident per CU)
@@ -2808,9 +2881,6 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   for (int k8 = 0; k8 < 8; ++k8)
     (void)hipFuncSetAttribute((const void*)f32_kernel(k8 & 4, (k8 & 1) | ((k8 & 2) << 1)),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  for (int k8 = 0; k8 < 8; ++k8)
-    (void)hipFuncSetAttribute((const void*)dual_kernel(k8 & 4, k8 & 3), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
@@ -2911,24 +2981,22 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   // against two (three: 33.4); the FP32 tree keeps two (one or three: neutral)
   ykbvh::Options bopt;
   bopt.max_leaf = kLeafCapF64;  // the FP64 kernel tests one sphere per leaf, without a loop
-  if (const char* e = std::getenv("YKGPU_BVH_BINS")) bopt.bins = std::max(2, std::min(256, std::atoi(e)));  // (A/B)
+  if (const char* e = ab_knob("YKGPU_BVH_BINS")) bopt.bins = std::max(2, std::min(256, std::atoi(e)));  // (A/B)
   // SAH over all three axes: 512-spp A/B 199.4 -> 198.3 ms (model: 5.51 -> 5.13 visits per segment)
   bopt.all_axes = true;
-  if (const char* e = std::getenv("YKGPU_BVH_ALLAXES")) bopt.all_axes = std::atoi(e) != 0;                  // (A/B)
-  const RenderKernel k64[3][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
-                                  {fp64_kernel(false, 4), fp64_kernel(true, 4)},
-                                  {dual_kernel(false, 0), dual_kernel(true, 0)}};
+  if (const char* e = ab_knob("YKGPU_BVH_ALLAXES")) bopt.all_axes = std::atoi(e) != 0;                  // (A/B)
+  const RenderKernel k64[2][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
+                                  {fp64_kernel(false, 4), fp64_kernel(true, 4)}};
   int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, kLeafCapF64, geo.data(), sizeof(SphereGeo),
                        sizeof(SphereGeo), k64);
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
   fopt.max_leaf = kLeafCapF32;  // the FP32 kernel's leaf loop is unrolled for two spheres
-  if (const char* e = std::getenv("YKGPU_BVH_ALLAXES_F32")) fopt.all_axes = std::atoi(e) != 0;  // (A/B; on: neutral)
+  if (const char* e = ab_knob("YKGPU_BVH_ALLAXES_F32")) fopt.all_axes = std::atoi(e) != 0;  // (A/B; on: neutral)
   fopt.radius_grow = 2.0 * (double)ykbvh::kF32Cone;
-  fopt.f32_big = std::getenv("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
-  const RenderKernel k32[3][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
-                                  {f32_kernel(false, 4), f32_kernel(true, 4)},
-                                  {f32_kernel(false, 0), f32_kernel(true, 0)}};  // (no dual FP32 kernel)
+  fopt.f32_big = ab_knob("YKGPU_F32_NO_BIG") == nullptr;  // (A/B: the cone bound alone)
+  const RenderKernel k32[2][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
+                                  {f32_kernel(false, 4), f32_kernel(true, 4)}};
   rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, kLeafCapF32, geo_f.data(), sizeof(float4),
                    sizeof(float4), k32);
   if (rc) return rc;

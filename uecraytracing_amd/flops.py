@@ -134,3 +134,90 @@ def implementation(st: dict) -> float:
             + lamb * IMPL["lambertian"] + metal * IMPL["metal"] + fuzz * IMPL["metal_fuzz"]
             + diel * IMPL["dielectric"] + sky * IMPL["sky"] + (lamb + metal) * IMPL["attenuation"]
             + st["samples"] * IMPL["sample"])
+
+
+# --- the VALU lane-op roofline: the path's whole work -----------
+# SURVEY §8(d) counts, beside the FP64 flops, the RNG's integer work.  ALGORITHMIC lane-ops are the
+# reference's own operators for the work done, one per C++ operator (an IEEE add / mul / divide /
+# conversion / compare, a 32-bit shift / xor / and / or / multiply / add), per lane:
+#   * the FP64 flops above (algorithmic(st));
+#   * mt19937 (random.hpp:43-151).  A sample's engine is seeded from its seed (x_i =
+#     1812433253 (x_{i-1} ^ x_{i-1} >> 30) + i, :69-81: >>, ^, *, + = 4 ops per step) and output j
+#     (j < 227) is temper(x_{j+397} ^ mix(x_j, x_{j+1})) (:114-131, :95-105).  The least work that
+#     yields the draws a sample makes: the walk to x_397 (397 steps) once, then per draw the next
+#     x_{j+397} (one step), the twisted word (mix: (a & U) | (b & L), >> 1, the odd select, two
+#     xors: 7) and the tempering (4 shifts, 2 ands, 4 xors: 10): 21 integer ops per word; plus
+#     generate_canonical's FP64 part per word (the u32 -> double conversion; per canonical of two
+#     words u0 + u1 2^32 (mul, add), / 2^64, >= 1: 3 ops per word).  A sample past draw 227 has
+#     its full engine seeded (623 steps) and twisted (624 words x 7 ops per twist, work[7]).
+#   * xor128 (random.hpp:18-41): 7 integer ops per word (<<, ^, >>, ^, >>, ^, ^), no seeding.
+# Classes, because the VALU issues them at different rates (tools/ubench.hip, 8 waves per SIMD):
+# FP64 (v_fma_f64's cost: ~4.4 SIMD cycles per wave-instruction), 32-bit multiplies
+# (v_mul_lo_u32, ~4.4), other 32-bit integer ops (v_xor_b32, ~2.5).  The PEAK of a mix is the
+# rate at which every SIMD would issue exactly that mix with all 64 lanes of every instruction
+# active: 64 x 1024 SIMDs x 2.4 GHz x N_total / sum_k N_k c_k.
+SEED_STEP_OPS = 4
+SEED_STEP_MULS = 1
+WALK_STEPS = 397
+DRAW_INT_OPS = 21       # one seeding step (4, one multiply) + the twisted word (7) + tempering (10)
+DRAW_MULS = 1
+WORD_F64_OPS = 3        # generate_canonical's conversion and arithmetic, per word
+TWIST_WORD_OPS = 7
+MT_STATE_WORDS = 624
+X128_WORD_OPS = 7
+CAMERA_F64_OPS = 24     # the start's jitter + camera ray (part of ALG_PER_SAMPLE, done by the warm-up)
+UBENCH_R05 = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                          "profiles", "r05_ubench.jsonl")
+
+
+UBENCH_R03D = os.path.join(os.path.dirname(UBENCH_EVIDENCE), "r03d_ubench.jsonl")
+
+
+def issue_costs(path: str = UBENCH_R05, fallback: str = UBENCH_R03D):
+    """SIMD cycles per wave64 instruction at 2.4 GHz of each op class, at the saturating 8 waves
+    per SIMD (tools/ubench.hip chip rows): {'f64', 'mul32', 'int32'} and the evidence file."""
+    src = path if os.path.exists(path) else fallback
+    rows = [r for r in ubench_rows(src) if r.get("waves_per_simd") == 8 and "chip_op" in r]
+    by = {r["chip_op"]: r["simd_cycles_per_instr_at_2400mhz"] for r in rows}
+    int32 = by.get("xor_b32", by["xor_shr_u32"] / 2)  # xor_shr_u32 issues two instructions
+    return {"f64": by["fma_f64"], "mul32": by["mul_lo_u32"], "int32": int32}, os.path.relpath(
+        src, os.path.dirname(os.path.dirname(src)))
+
+
+def lane_ops(st: dict, engine: str = "mt19937") -> dict:
+    """Algorithmic lane-ops of one counted call by class and by kernel (the seed-walk kernel
+    yk_mt_warmup: the walk, the start's draws and camera ray; the render: the rest)."""
+    n = st["samples"]
+    w = st["work"]
+    words, swords, twists, fb = w[5], w[6], w[7], st["mt_fallbacks"]
+    f64_all = algorithmic(st) + WORD_F64_OPS * words
+    if engine == "xor128":  # no warm-up kernel: the render does the whole start
+        warm = {"f64": 0.0, "mul32": 0.0, "int32": 0.0}
+        rend = {"f64": f64_all, "mul32": 0.0, "int32": X128_WORD_OPS * words}
+        return {"warmup": warm, "render": rend}
+    walk_int = n * WALK_STEPS * (SEED_STEP_OPS - SEED_STEP_MULS)
+    warm = {"f64": n * CAMERA_F64_OPS + WORD_F64_OPS * swords,
+            "mul32": n * WALK_STEPS * SEED_STEP_MULS + swords * DRAW_MULS,
+            "int32": walk_int + swords * (DRAW_INT_OPS - DRAW_MULS)}
+    rw = words - swords
+    rend = {"f64": f64_all - warm["f64"],
+            "mul32": rw * DRAW_MULS + fb * (MT_STATE_WORDS - 1) * SEED_STEP_MULS,
+            "int32": rw * (DRAW_INT_OPS - DRAW_MULS) + fb * (MT_STATE_WORDS - 1) * (SEED_STEP_OPS - SEED_STEP_MULS)
+                     + twists * MT_STATE_WORDS * TWIST_WORD_OPS}
+    return {"warmup": warm, "render": rend}
+
+
+def mix_peak(mix: dict, costs: dict, simds: int = 1024, ghz: float = 2.4) -> float:
+    """Lane-ops/s at which the chip issues this mix with every lane of every instruction active."""
+    tot = sum(mix.values())
+    cyc = sum(mix[k] * costs[k] for k in mix) / 64.0  # SIMD cycles for the mix
+    return tot / cyc * simds * ghz * 1e9 if cyc else 0.0
+
+
+def lane_op_roofline(ops: dict, seconds: float, costs: dict) -> dict:
+    tot = sum(ops.values())
+    peak = mix_peak(ops, costs)
+    ach = tot / seconds if seconds > 0 else 0.0
+    return {"algorithmic": round(tot), "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
+            "unit": "T lane-ops/s", "frac": round(ach / peak, 5) if peak else None,
+            "mix": {k: round(v / tot, 4) if tot else 0.0 for k, v in ops.items()}}

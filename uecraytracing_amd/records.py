@@ -122,6 +122,8 @@ class RenderStats(ctypes.Structure):
         ("device_bytes", ctypes.c_uint64),
         ("call_bytes", ctypes.c_uint64),
         ("sclk_mhz", ctypes.c_double),
+        ("launch_spp", ctypes.c_uint32),  # ABI 11
+        ("mem_shrinks", ctypes.c_uint32),
     ]
 
     def as_dict(self):
@@ -136,7 +138,7 @@ class RenderStats(ctypes.Structure):
 assert ctypes.sizeof(Sphere) == 80
 assert ctypes.sizeof(Camera) == 19 * 8
 assert ctypes.sizeof(RenderParams) == 88
-assert ctypes.sizeof(RenderStats) == 336
+assert ctypes.sizeof(RenderStats) == 344
 
 
 def image_height_for(width: int) -> int:
