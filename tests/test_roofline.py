@@ -108,3 +108,78 @@ def test_peak_falls_back_to_the_datasheet_without_the_ubench_file(tmp_path):
     peak, ev = flops.fp64_valu_peak(str(tmp_path / "absent.jsonl"))
     assert peak == flops.SPEC_FP64_VALU_TFLOPS
     assert "datasheet" in ev["source"] and "absent" in ev["note"]
+
+
+def test_lane_op_model_counts_the_rng_work():
+    """SURVEY §8(d)'s algorithmic work includes the RNG's integer ops: the
+    seed walk (397 steps of 4 ops per sample) dominates a sample's lane-ops, the per-word ops
+    follow the words drawn, and the warm-up / render split adds up to the whole."""
+    st = {"samples": 1000, "segments": 2100, "sphere_tests": 4000, "sqrt_calls": 1300, "newton_calls": 3000,
+          "newton_iters": 3000, "mt_fallbacks": 0, "work": [2000, 900, 300, 100, 200, 11000, 4400, 0]}
+    lo = flops.lane_ops(st)
+    walk = st["samples"] * flops.WALK_STEPS * flops.SEED_STEP_OPS
+    assert lo["warmup"]["mul32"] + lo["warmup"]["int32"] == walk + st["work"][6] * flops.DRAW_INT_OPS
+    assert lo["render"]["mul32"] + lo["render"]["int32"] == (st["work"][5] - st["work"][6]) * flops.DRAW_INT_OPS
+    f64 = flops.algorithmic(st) + flops.WORD_F64_OPS * st["work"][5]
+    assert abs(lo["warmup"]["f64"] + lo["render"]["f64"] - f64) < 1e-6
+    # the integer work outweighs the FP64 work per sample, as the verdict estimated
+    tot = {k: lo["warmup"][k] + lo["render"][k] for k in lo["render"]}
+    assert tot["mul32"] + tot["int32"] > 4 * tot["f64"]
+    # a mix's peak lies between its classes' peaks; all-FP64 is the v_fma_f64 instruction rate
+    costs, _ = flops.issue_costs()
+    p64 = flops.mix_peak({"f64": 1.0, "mul32": 0.0, "int32": 0.0}, costs)
+    assert abs(p64 - 64 * 1024 * 2.4e9 / costs["f64"]) / p64 < 1e-9
+    pint = flops.mix_peak({"f64": 0.0, "mul32": 0.0, "int32": 1.0}, costs)
+    assert p64 < flops.mix_peak(tot, costs) < pint
+
+
+def test_issue_costs_are_measured_rates():
+    """profiles/r05_ubench.jsonl (tools/ubench.hip at 8 waves per SIMD): a plain 32-bit op issues
+    at ~2.5 SIMD cycles per wave-instruction, the 32-bit multiply and the FP64 FMA at ~4.4, and the
+    seed walk's step (shift, xor, 64-bit multiply-add) costs their sum."""
+    costs, src = flops.issue_costs()
+    assert "r05_ubench" in src
+    assert 2.0 < costs["int32"] < 3.0 and 3.8 < costs["mul32"] < 5.0 and 3.8 < costs["f64"] < 5.0
+    rows = {r["chip_op"]: r for r in flops.ubench_rows(flops.UBENCH_R05)
+            if r.get("waves_per_simd") == 8 and "chip_op" in r}
+    walk = rows["walk_step"]["simd_cycles_per_instr_at_2400mhz"]
+    parts = 2 * rows["xor_b32"]["simd_cycles_per_instr_at_2400mhz"] + rows["mad_u64_u32"]["simd_cycles_per_instr_at_2400mhz"]
+    assert abs(walk / parts - 1) < 0.1
+
+
+def test_lane_op_reconciliation_with_the_pmc_counters():
+    """profiles/pmc_lane_ops.json (tools/gpu_lane_ops.sh): the render's executed lane-ops from
+    the one-lane count agree with the PMC-derived ones (SQ_INSTS_VALU x 64 x lane utilisation) of
+    the same binary within 10%, and of the production instance within 10% once the counting
+    instance's wave-instruction ratio carries it over; the warm-up's ISA model agrees with its PMC figure
+    within 10%; the algorithmic lane-ops are a part of what executes."""
+    f = os.path.join(PROF, "pmc_lane_ops.json")
+    if not os.path.exists(f):
+        pytest.skip("no lane-op reconciliation in profiles/")
+    rec = json.load(open(f))
+    r, w = rec["render"], rec["warmup"]
+    assert rec["images_equal"]
+    assert abs(r["model_over_pmc_counting"] - 1) < 0.10
+    assert abs(r["model_over_pmc_production"] - 1) < 0.10
+    assert abs(w["model_over_pmc"] - 1) < 0.10
+    assert r["lane_utilization"]["one_lane_C"] < 1.5 / 64 < 0.3 < r["lane_utilization"]["production_A"]
+    assert 0 < r["algorithmic_share_of_executed"] < 1 and 0 < w["algorithmic_share_of_executed"] < 1.5
+
+
+def test_bench_line_carries_the_lane_op_roofline():
+    b = json.load(open(latest_bench()))
+    vo = b["roofline"].get("valu_ops")
+    if vo is None:
+        pytest.skip("bench line from before the lane-op roofline")
+    for k in ("render", "warmup", "step"):
+        x = vo[k]
+        assert set(("algorithmic", "achieved", "peak", "frac")) <= set(x)
+        assert 0 < x["frac"] < 1
+        assert abs(x["achieved"] / x["peak"] - x["frac"]) / x["frac"] < 0.01
+    # the step's work is both kernels' work
+    per_step = vo["render"]["algorithmic"] * b["roofline"]["launches_per_step"] + \
+        vo["warmup"]["algorithmic"] * b["roofline"]["launches_per_step"]
+    assert abs(per_step / vo["step"]["algorithmic"] - 1) < 0.01
+    if b["roofline"]["hbm"].get("traffic_per_sample"):
+        h = b["roofline"]["hbm"]
+        assert abs(h["traffic_per_sample"] / h["algorithmic_bytes_per_sample"] / h["traffic_over_algorithmic"] - 1) < 0.01

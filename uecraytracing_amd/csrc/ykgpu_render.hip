@@ -139,6 +139,19 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 #define YK_CLAIM 512
 #endif
 constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
+// ... and near the end of a launch's slots: when fewer than kClaimTailFactor x kClaim slots per
+// wave of the grid remain (as the wave last saw the counter), a wave claims kClaimTail slots at a
+// time.  A wave's reserve holds up to kClaim slots (8 samples per lane) when the counter runs
+// out, so with full claims to the end some waves still have ~8 samples per lane of work while
+// others have none, and every launch drains for that long (0: full claims to the end).
+#ifndef YK_CLAIM_TAIL
+#define YK_CLAIM_TAIL 64
+#endif
+#ifndef YK_CLAIM_TAIL_FACTOR
+#define YK_CLAIM_TAIL_FACTOR 2
+#endif
+constexpr uint32_t kClaimTail = YK_CLAIM_TAIL, kClaimTailFactor = YK_CLAIM_TAIL_FACTOR;
+static_assert(kClaimTail == 0 || (kClaimTail >= 64 && kClaimTail <= YK_CLAIM), "a tail claim serves a whole wave");
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
@@ -598,10 +611,16 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
   const unsigned long long m = __ballot(!in_path);
   if (m) {
     const uint32_t need = (uint32_t)__popcll(m);
-    uint32_t fresh = 0;
+    uint32_t fresh = 0, csize = kClaim;
     if (res_left < need) {
+      if (kClaimTail) {
+        // res_base + res_left: where the counter stood after this wave's last claim
+        const uint32_t seen = res_base + res_left;
+        const uint32_t tail = gridDim.x * (blockDim.x >> 6) * kClaim * kClaimTailFactor;
+        if (seen >= ka.nsl || ka.nsl - seen < tail) csize = kClaimTail;
+      }
       const int leader = __ffsll((long long)m) - 1;
-      if ((int)lane == leader) fresh = atomicAdd(ka.pixel_counter, kClaim);
+      if ((int)lane == leader) fresh = atomicAdd(ka.pixel_counter, csize);
       fresh = __shfl(fresh, leader);
     }
     if (!in_path) {
@@ -610,7 +629,7 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
     }
     if (res_left < need) {
       res_base = fresh + (need - res_left);
-      res_left = kClaim - (need - res_left);
+      res_left = csize - (need - res_left);
     } else {
       res_base += need;
       res_left -= need;
