@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
 #include <random>
 #include <vector>
 
@@ -197,10 +198,11 @@ int main(int argc, char** argv) {
   std::uniform_real_distribution<double> U(0, 1);
   std::vector<std::pair<V, V>> seg;
   std::vector<int> seg_depth;
-  const int W = 192, H = 108;
+  const int W = getenv("YKSIM_W") ? atoi(getenv("YKSIM_W")) : 192, H = W * 9 / 16;
+  const int SPP = getenv("YKSIM_SPP") ? atoi(getenv("YKSIM_SPP")) : 2;
   for (int y = 0; y < H; ++y)
     for (int x = 0; x < W; ++x)
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < SPP; ++s) {
         double u = (x + U(rng)) / W, v = (H - y - 1 + U(rng)) / H;
         V o = ld(cam.origin);
         V d = sub(add(add(ld(cam.lower_left_corner), mul(ld(cam.horizontal), u)), mul(ld(cam.vertical), v)), o);
@@ -263,8 +265,180 @@ int main(int argc, char** argv) {
           idx.push_back(seg.size());
           seg.push_back({o, d});
         }
+    // YKSIM_PRIMARY_SHUFFLE=1: the same camera rays in random waves (coherence vs ray kind)
+    if (getenv("YKSIM_PRIMARY_SHUFFLE")) std::shuffle(idx.begin(), idx.end(), rng);
   }
   auto rcp = [](float x) { return std::fabs(x) > 1e-30f ? 1.0f / x : std::copysign(1e30f, x); };
+  // traversal cost of one trip of the shipped (if/else) loop over an arbitrary set of rays
+  auto trav_cost = [&](const std::vector<std::pair<V, V>>& rays) {
+    std::vector<Lane> lanes(rays.size());
+    for (size_t k = 0; k < rays.size(); ++k) {
+      Lane& L = lanes[k];
+      L.o = rays[k].first;
+      L.d = rays[k].second;
+      L.a = dot(L.d, L.d);
+      L.ix = rcp((float)L.d.x), L.iy = rcp((float)L.d.y), L.iz = rcp((float)L.d.z);
+      L.node = M.root;
+    }
+    double cost = 0;
+    for (;;) {
+      bool any_v = false;
+      int max_cnt = 0, max_dpos = 0, act = 0;
+      for (auto& L : lanes) {
+        if (L.done) continue;
+        ++act;
+        if (L.node >= 0) {
+          any_v = true;
+          M.visit(L);
+          if (L.node == kDone) L.done = true;
+        } else {
+          auto [cnt, dp] = M.leaf(L, L.node);
+          max_cnt = std::max(max_cnt, cnt);
+          max_dpos = std::max(max_dpos, dp);
+          M.pop(L);
+          if (L.node == kDone) L.done = true;
+        }
+      }
+      if (!act) break;
+      cost += c_trip + c_visit * any_v + c_leaf * max_cnt + c_disc * max_dpos;
+    }
+    return cost;
+  };
+  // YKSIM_BURST="other T Q": one wave's refill policy over the slot stream (slot order = the
+  // kernel's: 8x8 pixel blocks, sample index outermost), every trip = the traversal of the active
+  // lanes' current segments + `other`.  T = 0: the shipped refill (every free lane takes the next
+  // slot each trip).  T > 0: park & burst — when at least T lanes are free (and the park queue,
+  // FIFO of capacity Q, has room for the active ones), the active lanes are parked and the wave
+  // starts 64 consecutive slots together (a coherent primary trip); otherwise free lanes take
+  // parked paths, and stay idle when there are none.
+  if (const char* bs = getenv("YKSIM_BURST")) {
+    double other = 957, T = 0, Q = 64;
+    sscanf(bs, "%lf %lf %lf", &other, &T, &Q);
+    std::vector<std::vector<size_t>> path((size_t)W * H * SPP);
+    {
+      size_t sidx = 0;
+      for (size_t i = 0; i < seg.size(); ++i) {
+        if (seg_depth[i] == 0 && i > 0) ++sidx;
+        path[sidx].push_back(i);
+      }
+    }
+    std::vector<size_t> slots;  // sample index per slot
+    // YKSIM_BLOCKMAJOR=1: a block's samples contiguous (block, sample, pixel) instead of
+    // (sample, block, pixel)
+    const bool bm = getenv("YKSIM_BLOCKMAJOR") != nullptr;
+    for (int s0 = 0; s0 < (bm ? 1 : SPP); ++s0)
+      for (int by = 0; by < H; by += 8)
+        for (int bx = 0; bx < W; bx += 8)
+          for (int s = bm ? 0 : s0; s < (bm ? SPP : s0 + 1); ++s)
+            for (int k = 0; k < 64; ++k) {
+              const int x = bx + k % 8, y = by + k / 8;
+              if (x < W && y < H) slots.push_back(((size_t)y * W + x) * SPP + s);
+            }
+    struct P { size_t q; int d; };
+    std::vector<P> lane(64, P{0, -1});  // d < 0: free
+    std::deque<P> park;
+    size_t next = 0;
+    double cost = 0, trips = 0, bursts = 0, lanes_active = 0;
+    for (;;) {
+      int nfree = 0;
+      for (auto& l : lane) nfree += l.d < 0;
+      const int nact = 64 - nfree;
+      if (T > 0 && nfree >= T && next < slots.size() && park.size() + nact <= Q) {
+        for (auto& l : lane)
+          if (l.d >= 0) park.push_back(l), l.d = -1;
+        for (auto& l : lane)
+          if (next < slots.size()) l = P{slots[next++], 0};
+        ++bursts;
+      } else {
+        for (auto& l : lane) {
+          if (l.d >= 0) continue;
+          if (T > 0) {
+            if (!park.empty()) l = park.front(), park.pop_front();
+          } else if (next < slots.size()) {
+            l = P{slots[next++], 0};
+          }
+        }
+      }
+      std::vector<std::pair<V, V>> rays;
+      for (auto& l : lane)
+        if (l.d >= 0) rays.push_back(seg[path[l.q][l.d]]);
+      if (rays.empty()) {
+        if (next >= slots.size() && park.empty()) break;
+        if (T > 0 && next < slots.size()) {  // nothing to run: burst regardless of T
+          for (auto& l : lane)
+            if (next < slots.size()) l = P{slots[next++], 0};
+          ++bursts;
+          continue;
+        }
+        continue;
+      }
+      cost += trav_cost(rays) + other;
+      trips += 1;
+      lanes_active += rays.size();
+      for (auto& l : lane)
+        if (l.d >= 0 && ++l.d >= (int)path[l.q].size()) l.d = -1;
+    }
+    printf("burst(other=%.0f, T=%.0f, Q=%.0f): per sample %.1f | trips %.0f, bursts %.0f, lanes per trip %.1f\n",
+           other, T, Q, cost / slots.size(), trips, bursts, lanes_active / trips);
+  }
+  // YKSIM_WAVESYNC=other: waves of 64 coherent samples (one 8x8 block, one sample index) traced in
+  // lockstep to their end, no refill: trip d holds the samples' depth-d segments; every trip also
+  // pays `other` for the rest of the loop (shading, path end, start, refill), whatever its lanes.
+  // Printed beside the shipped refill loop's cost per sample (random waves of 64 segments) and
+  // the split (coherent primary waves + random bounce waves)
+  if (const char* ws = getenv("YKSIM_WAVESYNC")) {
+    const double other = atof(ws);
+    std::vector<std::vector<size_t>> path((size_t)W * H * SPP);  // segment indices per sample, (y, x, s) order
+    {
+      size_t sidx = 0;
+      for (size_t i = 0; i < seg.size(); ++i) {
+        if (seg_depth[i] == 0 && i > 0) ++sidx;
+        path[sidx].push_back(i);
+      }
+    }
+    double sync = 0, nsamp = 0, prim = 0, bounce = 0, mixed = 0, nb = 0;
+    std::vector<size_t> bidx;
+    for (int s = 0; s < 2; ++s)
+      for (int by = 0; by < H; by += 8)
+        for (int bx = 0; bx < W; bx += 8) {
+          std::vector<size_t> smp;
+          for (int k = 0; k < 64; ++k) {
+            const int x = bx + k % 8, y = by + k / 8;
+            if (x < W && y < H) smp.push_back(((size_t)y * W + x) * SPP + s);
+          }
+          if (smp.size() < 64) continue;
+          for (int d = 0;; ++d) {
+            std::vector<std::pair<V, V>> rays;
+            for (size_t q : smp)
+              if ((int)path[q].size() > d) rays.push_back(seg[path[q][d]]);
+            if (rays.empty()) break;
+            const double c = trav_cost(rays) + other;
+            sync += c;
+            if (d == 0) prim += c;
+          }
+          for (size_t q : smp)
+            for (size_t k = 1; k < path[q].size(); ++k) bidx.push_back(path[q][k]);
+          nsamp += smp.size();
+        }
+    std::shuffle(bidx.begin(), bidx.end(), rng);
+    for (size_t g = 0; g + 64 <= bidx.size(); g += 64) {
+      std::vector<std::pair<V, V>> rays;
+      for (int k = 0; k < 64; ++k) rays.push_back(seg[bidx[g + k]]);
+      bounce += trav_cost(rays) + other;
+      nb += 64;
+    }
+    for (size_t g = 0; g + 64 <= idx.size(); g += 64) {
+      std::vector<std::pair<V, V>> rays;
+      for (int k = 0; k < 64; ++k) rays.push_back(seg[idx[g + k]]);
+      mixed += trav_cost(rays) + other;
+    }
+    const double segs_per_sample = (double)seg.size() / (W * H * 2);
+    const double mixed_ps = mixed / (idx.size() / 64) / 64 * segs_per_sample;
+    const double split_ps = prim / nsamp + bounce / nb * (bidx.size() / nsamp);
+    printf("wavesync(other=%.0f): per sample: refill loop (random waves) %.1f | lockstep coherent waves %.1f (%.3fx) | "
+           "coherent primary waves + random bounce waves %.1f (%.3fx)\n",
+           other, mixed_ps, sync / nsamp, sync / nsamp / mixed_ps, split_ps, split_ps / mixed_ps);
+  }
 
   printf("%s n=%u leaf<=%u wide nodes %zu depth %u | %zu segments | weights visit %.0f leaf %.0f disc %.0f trip %.0f\n",
          scene, n, opt.max_leaf, M.wide.size(), wd, seg.size(), c_visit, c_leaf, c_disc, c_trip);
