@@ -793,7 +793,9 @@ void yk_render_persistent(KernelArgs ka) {
   // survivors compacted so far (wave-uniform)
   uint32_t rbase = 0, rleft = 0, rreg = 0, rrank = 0;
   bool got = false;  // kBounce: this lane took a continuation record this trip
-  uint32_t touch = 0;  // (YK_PRIMARY_TOUCH)
+#if YK_PRIMARY_TOUCH
+  uint32_t touch = 0;
+#endif
 
   for (;;) {
     // ---- refill (claim_slots): lanes without a path take the next sample slots
