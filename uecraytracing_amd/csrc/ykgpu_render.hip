@@ -157,6 +157,36 @@ constexpr uint32_t kClaimTail = YK_CLAIM_TAIL, kClaimTailFactor = YK_CLAIM_TAIL_
 #define YK_PRIMARY_TOUCH 0
 #endif
 static_assert(kClaimTail == 0 || (kClaimTail >= 64 && kClaimTail <= YK_CLAIM), "a tail claim serves a whole wave");
+// The fused first-segment render (kMode 32): waves [0, kFusedProducers) of a
+// workgroup render first segments region by region and queue the survivors' records in LDS; the
+// others render bounces from that queue (a wave with every lane free and an empty queue renders a
+// region itself).  Producers pause while more than kQueueHi chunks wait.
+#ifndef YK_FUSED_PRODUCERS
+#define YK_FUSED_PRODUCERS 3
+#endif
+#ifndef YK_QUEUE_HI
+#define YK_QUEUE_HI 32
+#endif
+#ifndef YK_FUSED_HELP
+#define YK_FUSED_HELP 0
+#endif
+// diagnostic builds (YK_FUSED_DIAG): ykgpu_get_stats diag[0..3] = producer-wave pauses (queue
+// long), waits of waves with nothing to render, consumer trips with free lanes and no chunk,
+// regions rendered by non-producer waves
+#ifdef YK_FUSED_DIAG
+#define YK_FDIAG(k) (lane == 0 ? (void)atomicAdd(&ka.counters[19 + (k)], 1ull) : (void)0)
+#else
+#define YK_FDIAG(k) ((void)0)
+#endif
+constexpr uint32_t kFusedProducers = YK_FUSED_PRODUCERS, kQueueHi = YK_QUEUE_HI;
+// the ready queue: chunks of <= 64 continuation records (a region's survivors in kClaim / 64
+// chunks at most); every wave of a 768-thread workgroup may push a region's chunks past kQueueHi
+constexpr uint32_t kQueueCap = 128;
+static_assert(kQueueHi + (YK_BLOCK / 64) * (YK_CLAIM / 64) <= kQueueCap, "the ready queue can overflow");
+struct ReadyQueue {
+  uint32_t head, tail, producing, pad;
+  unsigned long long ent[kQueueCap];  // (first record << 32) | (count << 1) | 1; 0: not published
+};
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
@@ -213,7 +243,7 @@ struct KernelArgs {
   uint2* meta;
   uint32_t* rcount;
   uint32_t* claim2;
-  uint32_t nreg, pad_s;
+  uint32_t nreg, lds_queue_off;  // lds_queue_off: the fused render's ReadyQueue in LDS
 };
 
 // Shader-clock probe of a launch: thread 0 of block 0 stores s_memtime (the shader clock) and
@@ -697,6 +727,140 @@ __device__ __forceinline__ bool claim_regions(const KernelArgs& ka, bool in_path
   return !in_path && !got && out;
 }
 
+// The fused render's ready queue (ReadyQueue, kMode 32).  Every wave of the workgroup is on this
+// CU, so workgroup-scope release / acquire order the records (global memory, this CU's L1 and its
+// XCD's L2) against the queue words in LDS.
+__device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Producer, every lane, after a region's last batch: its `count` survivors (records first ..
+// first + count - 1) as chunks of <= 64, published after the records
+__device__ __forceinline__ void queue_push(ReadyQueue* q, uint32_t first, uint32_t count, uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) {
+    for (uint32_t k = 0; k < count; k += 64u) {
+      const uint32_t t = __hip_atomic_fetch_add(&q->tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const unsigned long long e =
+          ((unsigned long long)(first + k) << 32) | ((unsigned long long)min(64u, count - k) << 1) | 1ull;
+      __hip_atomic_store(&q->ent[t % kQueueCap], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __hip_atomic_fetch_sub(&q->producing, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// Consumer, lane 0: the oldest published chunk, or 0 (queue empty, its head not yet published, or
+// another wave took it first)
+__device__ __forceinline__ unsigned long long queue_pop(ReadyQueue* q) {
+  const uint32_t h = lds_load(&q->head);
+  if (h == lds_load(&q->tail)) return 0;
+  const unsigned long long e = __hip_atomic_load(&q->ent[h % kQueueCap], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (!e) return 0;
+  uint32_t hx = h;
+  if (!__hip_atomic_compare_exchange_strong(&q->head, &hx, h + 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP))
+    return 0;
+  __hip_atomic_store(&q->ent[h % kQueueCap], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return e;
+}
+
+// Refill of the fused render (kMode 32).  Wave-uniform state: `producing` (the wave renders the
+// first segments of region rbase .. in batches of 64 slots: every lane starts slot rbase + lane),
+// the record reserve (res_base, res_left) and pool_done (the launch's slot counter ran out).  A
+// wave that is not producing serves its free lanes from the reserve and then from the queue; one
+// with every lane free and nothing in reserve takes a region when it may (producer waves while
+// at most kQueueHi chunks wait, the others when the queue is empty).  got: this lane took record
+// `idx`.  Returns true when the wave leaves: no path, no region left and no producer that could
+// still queue one.
+__device__ __forceinline__ bool fused_refill(const KernelArgs& ka, ReadyQueue* q, bool in_path, uint32_t lane,
+                                             bool prod_role, uint32_t& idx, bool& got, bool& producing,
+                                             uint32_t& rbase, uint32_t& rleft, uint32_t& rreg, uint32_t& rrank,
+                                             uint32_t& res_base, uint32_t& res_left, bool& pool_done) {
+  got = false;
+  if (producing) {
+    idx = rbase + lane;
+    return false;
+  }
+  const unsigned long long m = __ballot(!in_path);
+  if (!m) return false;
+  if (m == ~0ull && res_left == 0 && !pool_done) {
+    uint32_t v = 0;  // 1 + the region's first slot; ~0: the slots ran out
+    if (lane == 0) {
+      const uint32_t len = lds_load(&q->tail) - lds_load(&q->head);
+      if (prod_role ? len < kQueueHi : len == 0) {
+        // counted as producing before the claim: a wave that finds the counter exhausted then
+        // also sees every region claimed before it as pushed or in progress
+        (void)__hip_atomic_fetch_add(&q->producing, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        const uint32_t fresh = atomicAdd(ka.pixel_counter, kClaim);
+        if (fresh < ka.nsl) {
+          v = fresh + 1u;
+        } else {
+          (void)__hip_atomic_fetch_sub(&q->producing, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          v = ~0u;
+        }
+      }
+    }
+    v = __shfl(v, 0);
+    if (v == ~0u) {
+      pool_done = true;
+    } else if (v) {
+      if (!prod_role) YK_FDIAG(3);
+      producing = true;
+      rbase = v - 1u;
+      rreg = rbase / kClaim;
+      rrank = 0;
+      rleft = min(kClaim, ka.nsl - rbase) / 64u;
+      idx = rbase + lane;
+      return false;
+    }
+  }
+  const uint32_t need = (uint32_t)__popcll(m);
+  uint32_t nb = 0, nleft = 0;
+  // (a producer wave takes no chunks while regions are left: it waits for the queue to shorten;
+  // YK_FUSED_HELP: it renders bounces from the queue meanwhile)
+  if (res_left < need && (YK_FUSED_HELP || !(prod_role && !pool_done))) {
+    unsigned long long e = 0;
+    if (lane == 0) e = queue_pop(q);
+    const uint32_t ehi = __shfl((uint32_t)(e >> 32), 0), elo = __shfl((uint32_t)e, 0);
+    if (elo) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the chunk's records after its entry
+      nb = ehi;
+      nleft = elo >> 1;
+    }
+  }
+  if (!in_path) {
+    const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (r < res_left) {
+      idx = res_base + r;
+      got = true;
+    } else if (r - res_left < nleft) {
+      idx = nb + (r - res_left);
+      got = true;
+    }
+  }
+  if (res_left < need) {
+    const uint32_t take = min(need - res_left, nleft);
+    res_base = nb + take;
+    res_left = nleft - take;
+  } else {
+    res_base += need;
+    res_left -= need;
+  }
+  if (__ballot(in_path || got)) {
+    if (!prod_role && res_left == 0 && __ballot(!in_path && !got)) YK_FDIAG(2);
+    return false;
+  }
+  // nothing to render this trip: leave once no chunk can come, else let the producers run
+  uint32_t done = 0;
+  if (lane == 0)
+    done = pool_done && lds_load(&q->producing) == 0 && lds_load(&q->head) == lds_load(&q->tail);
+  if (__shfl(done, 0)) return true;
+  YK_FDIAG(prod_role && !pool_done ? 0 : 1);
+  __builtin_amdgcn_s_sleep(4);
+  return false;
+}
+
 using RenderKernel = void (*)(KernelArgs);
 
 // YK_SPLIT (Makefile): 0 — every kernel in this translation unit (the A/B variants of
@@ -732,8 +896,9 @@ void yk_render_persistent(KernelArgs ka) {
   constexpr bool kCount = (kMode & 1) != 0;
   constexpr bool kRandomSeed = (kMode & 2) != 0;
   using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
-  constexpr bool kPrimary = (kMode & 8) != 0, kBounce = (kMode & 16) != 0;
-  static_assert(!((kPrimary || kBounce) && ((kMode & 7) != 0)), "the split has production mt19937 instances only");
+  constexpr bool kPrimary = (kMode & 8) != 0, kBounce = (kMode & 16) != 0, kFused = (kMode & 32) != 0;
+  static_assert(!((kPrimary || kBounce || kFused) && ((kMode & 7) != 0)), "the split has production mt19937 instances only");
+  static_assert(!kFused || kSceneInLds, "the fused render's queue is in LDS beside the scene");
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -753,6 +918,10 @@ void yk_render_persistent(KernelArgs ka) {
     for (int k = 0; k < 5; ++k) {
       uint4* dst = (uint4*)(smem + off[k]);
       for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlk) dst[i] = src[k][i];
+    }
+    if constexpr (kFused) {
+      uint32_t* const qw = (uint32_t*)(smem + ka.lds_queue_off);
+      for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(ReadyQueue) / 4); i += kBlk) qw[i] = 0;
     }
     __syncthreads();
     nodes = smem;
@@ -793,6 +962,11 @@ void yk_render_persistent(KernelArgs ka) {
   // survivors compacted so far (wave-uniform)
   uint32_t rbase = 0, rleft = 0, rreg = 0, rrank = 0;
   bool got = false;  // kBounce: this lane took a continuation record this trip
+  // kFused: this wave renders a region's first segments now (wave-uniform); the launch's slots ran
+  // out; the wave is one of the workgroup's producers; the ready queue
+  bool producing = false, pool_done = false;
+  const bool prod_role = (threadIdx.x >> 6) < kFusedProducers;
+  ReadyQueue* const rq = (ReadyQueue*)(smem + ka.lds_queue_off);
 #if YK_PRIMARY_TOUCH
   uint32_t touch = 0;
 #endif
@@ -821,6 +995,10 @@ void yk_render_persistent(KernelArgs ka) {
 #endif
     } else if constexpr (kBounce) {
       if (claim_regions(ka, in_path, lane, slot, got, res_base, res_left)) break;
+    } else if constexpr (kFused) {
+      if (fused_refill(ka, rq, in_path, lane, prod_role, slot, got, producing, rbase, rleft, rreg, rrank, res_base,
+                       res_left, pool_done))
+        break;
     } else if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) {
       YK_STAMPS_EXHAUSTED(ka.counters);
       break;
@@ -836,7 +1014,9 @@ void yk_render_persistent(KernelArgs ka) {
     // included, has a record, so the read is in bounds.
     uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0}, rq3 = {0, 0, 0, 0};
     uint2 meta = {0, 0};
-    if constexpr (kBounce) {
+    // the wave renders bounces from continuation records (kBounce; kFused when not producing)
+    const bool from_rec = kBounce || (kFused && !producing);
+    if (from_rec) {
       // a continuation record (compacted index `slot`) and its (slot, seed), loaded together
       start = start && got;
       if (start) {
@@ -865,7 +1045,7 @@ void yk_render_persistent(KernelArgs ka) {
       }
       start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
-    if constexpr (kBounce) {
+    if constexpr (kBounce || kFused) if (from_rec) {
       if (start) {
         slot = meta.x;
         StartRec r;
@@ -908,22 +1088,24 @@ void yk_render_persistent(KernelArgs ka) {
       // seed (uint32 wrap, source.cpp:154-158)
       const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
       bool pre = false;
-      if constexpr (std::is_same<Gen, ykd::MtLane>::value && !kBounce) {
-        StartRec r;  // (loaded above with the pixel)
-        __builtin_memcpy((char*)&r, &rq0, 16);
-        __builtin_memcpy((char*)&r + 16, &rq1, 16);
-        __builtin_memcpy((char*)&r + 32, &rq2, 16);
-        __builtin_memcpy((char*)&r + 48, &rq3, 16);
-        pre = r.j != kNoStart;
-        if (pre) {
-          if (kCount) n_swords += r.j;
-          g.seed = seed;  // (the scratch engine's seeding needs it)
-          g.a0 = r.a0;
-          g.a1 = r.a1;
-          g.b = r.b;
-          g.j = r.j;
-          o = v3{r.ox, r.oy, r.oz};
-          d = v3{r.dx, r.dy, r.dz};
+      if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
+        if (!from_rec) {
+          StartRec r;  // (loaded above with the pixel)
+          __builtin_memcpy((char*)&r, &rq0, 16);
+          __builtin_memcpy((char*)&r + 16, &rq1, 16);
+          __builtin_memcpy((char*)&r + 32, &rq2, 16);
+          __builtin_memcpy((char*)&r + 48, &rq3, 16);
+          pre = r.j != kNoStart;
+          if (pre) {
+            if (kCount) n_swords += r.j;
+            g.seed = seed;  // (the scratch engine's seeding needs it)
+            g.a0 = r.a0;
+            g.a1 = r.a1;
+            g.b = r.b;
+            g.j = r.j;
+            o = v3{r.ox, r.oy, r.oz};
+            d = v3{r.dx, r.dy, r.dz};
+          }
         }
       }
       if (!pre) {
@@ -1320,7 +1502,7 @@ void yk_render_persistent(KernelArgs ka) {
     }
     YK_STAMP(4);
 
-    if constexpr (kPrimary) {
+    if constexpr (kPrimary || kFused) if (kPrimary || producing) {
 #if YK_PRIMARY_TOUCH
       asm volatile("" ::"v"(touch));
 #endif
@@ -1343,7 +1525,14 @@ void yk_render_persistent(KernelArgs ka) {
       }
       rrank += (uint32_t)__popcll(hm);
       rbase += 64u;
-      if (--rleft == 0 && lane == 0) ka.rcount[rreg] = rrank;
+      if (--rleft == 0) {
+        if constexpr (kFused) {
+          queue_push(rq, rreg * kClaim, rrank, lane);
+          producing = false;
+        } else if (lane == 0) {
+          ka.rcount[rreg] = rrank;
+        }
+      }
     }
 
     if (ended) {
@@ -1410,6 +1599,8 @@ RenderKernel fp64_kernel(bool lds, int mode) {
 RenderKernel split_kernel(bool bounce) {
   return bounce ? yk_render_persistent<true, 16> : yk_render_persistent<true, 8>;
 }
+// ... and the fused render: both in one kernel, the hand-over through the workgroup's LDS queue
+RenderKernel fused_kernel() { return yk_render_persistent<true, 32>; }
 
 #endif  // YK_SPLIT != 2
 
@@ -2282,11 +2473,12 @@ constexpr uint32_t kLaunchesPerCall = YK_LAUNCHES_PER_CALL;
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
 // The first-segment split: FP64 mt19937 production renders with the scene in LDS run
 // every sample's first segment in coherent batches (kPrimary) and the rest from continuation
-// records (kBounce); 0: one persistent kernel for the whole path, as before round 5
+// records (kBounce); 2: both in one kernel, the hand-over through an LDS queue per workgroup
+// (kFused); 0: one persistent kernel for the whole path, as before round 5
 #ifndef YK_PRIMARY_SPLIT
 #define YK_PRIMARY_SPLIT 0
 #endif
-constexpr bool kPrimarySplit = YK_PRIMARY_SPLIT != 0;
+constexpr bool kPrimarySplit = YK_PRIMARY_SPLIT != 0, kPrimaryFused = YK_PRIMARY_SPLIT == 2;
 // Under memory pressure (launch()): launches shrink down to this many sample slots before a call
 // fails with YK_ERR_NOMEM, and the rings leave kMemReserve of the device free
 constexpr uint64_t kMemFloorSlots = 1ull << 24;
@@ -2377,6 +2569,11 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride)
 // Render streams get the device's top priority (YKGPU_RENDER_PRIO=0: default priority, A/B): when
 // a launch drains, the queued warm-up and reduce blocks would otherwise take the CUs it frees
 // before the next launch's workgroups (one per CU, 768 threads and most of the LDS) fit.
+// the reduce stream at the render streams' priority (A/B: a reduce that shares the CUs with a
+// warm-up's grid can take several times its ~0.9 ms, and render c + 2 waits for it)
+#ifndef YK_REDUCE_PRIO
+#define YK_REDUCE_PRIO 0
+#endif
 hipError_t create_render_stream(hipStream_t* s) {
   int least = 0, greatest = 0;
   const char* e = ab_knob("YKGPU_RENDER_PRIO");
@@ -2580,9 +2777,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
                      !(p->flags & (YK_FLAG_COUNT_WORK | YK_FLAG_TRACE_RAYS | YK_FLAG_ONE_LANE)) &&
                      p->seed_mode == YK_SEED_COUNTER && p->max_depth >= 1;
   const size_t nreg_max = ((size_t)nps * K + kClaim - 1) / kClaim;
+  // the fused render's queue goes after the stacks (when the CU's LDS has room for it)
+  const uint32_t queue_off = (plan.lds_bytes + 15u) & ~15u;
+  const bool fused = split && kPrimaryFused && queue_off + sizeof(ReadyQueue) <= 160u * 1024u;
   if (split) {
     if ((rc = grow(ctx->d_meta, ctx->meta_cap, (size_t)kWarmRing * nps * K, sizeof(uint2)))) return rc;
-    if ((rc = grow(ctx->d_rcount, ctx->rcount_cap, (size_t)kWarmRing * nreg_max, sizeof(uint32_t)))) return rc;
+    if (!fused && (rc = grow(ctx->d_rcount, ctx->rcount_cap, (size_t)kWarmRing * nreg_max, sizeof(uint32_t))))
+      return rc;
   }
   KernelArgs ka;
   ka.cam = ctx->cam;
@@ -2646,7 +2847,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.meta = nullptr;
   ka.rcount = nullptr;
   ka.claim2 = nullptr;
-  ka.nreg = ka.pad_s = 0;
+  ka.nreg = ka.lds_queue_off = 0;
 
   ka.counters = ctx->d_stats;
   ka.trace = ctx->d_trace;
@@ -2843,11 +3044,16 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       // every sample's first segment in coherent batches, then the rest from its hand-over records,
       // on the same stream (the bounce kernel reads what the primary kernel wrote)
       ka.meta = ctx->d_meta + (size_t)(g % kWarmRing) * nps * K;
-      ka.rcount = ctx->d_rcount + (size_t)(g % kWarmRing) * nreg_max;
-      ka.nreg = (uint32_t)(((uint64_t)nsl + kClaim - 1) / kClaim);
-      hipLaunchKernelGGL(split_kernel(false), dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
-      YK_HIP(hipGetLastError());
-      hipLaunchKernelGGL(split_kernel(true), dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
+      if (fused) {
+        ka.lds_queue_off = queue_off;
+        hipLaunchKernelGGL(fused_kernel(), dim3(grid), dim3(block), queue_off + sizeof(ReadyQueue), rs, ka);
+      } else {
+        ka.rcount = ctx->d_rcount + (size_t)(g % kWarmRing) * nreg_max;
+        ka.nreg = (uint32_t)(((uint64_t)nsl + kClaim - 1) / kClaim);
+        hipLaunchKernelGGL(split_kernel(false), dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
+        YK_HIP(hipGetLastError());
+        hipLaunchKernelGGL(split_kernel(true), dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
+      }
     } else if (f32)
       hipLaunchKernelGGL(f32_kernel(plan.in_lds, (count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(block),
                          plan.lds_bytes, rs, ka);
@@ -2895,7 +3101,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     cb += (uint64_t)kColRing * nps * K * kColStride * sizeof(double) + (x128 ? 0 : (uint64_t)kWarmRing * nps * K * welem);
     cb += (nlaunch > 1 ? (uint64_t)nps * 3 * sizeof(double) : 0) + (uint64_t)nps * sizeof(uint32_t);
     cb += 2ull * nlaunch * sizeof(uint32_t) + kCounters * sizeof(unsigned long long);
-    if (split) cb += (uint64_t)kWarmRing * nps * K * sizeof(uint2) + kWarmRing * nreg_max * sizeof(uint32_t);
+    if (split) cb += (uint64_t)kWarmRing * nps * K * sizeof(uint2) + (fused ? 0 : kWarmRing * nreg_max * sizeof(uint32_t));
     if (!x128) cb += 2 * lanes * ykd::kMtN * sizeof(uint32_t);
     cb += 2 * lanes * std::max(1u, p->max_depth > kStackRegs ? p->max_depth : 1u) * sizeof(uint16_t);
     const uint64_t npix = (uint64_t)p->row_count * tile_width(p);
@@ -3114,9 +3320,11 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   for (bool bounce : {false, true})
     (void)hipFuncSetAttribute((const void*)split_kernel(bounce), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
+  (void)hipFuncSetAttribute((const void*)fused_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
+      (YK_REDUCE_PRIO ? create_render_stream(&ctx->red) : hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking)) !=
+          hipSuccess ||
       create_render_stream(&ctx->alt) != hipSuccess || create_render_stream(&ctx->ren) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
