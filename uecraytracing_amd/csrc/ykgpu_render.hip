@@ -151,42 +151,7 @@ constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
 #define YK_CLAIM_TAIL_FACTOR 2
 #endif
 constexpr uint32_t kClaimTail = YK_CLAIM_TAIL, kClaimTailFactor = YK_CLAIM_TAIL_FACTOR;
-// the first-segment split's primary kernel touches the next batch's start records at a batch's
-// start (their latency passes under the batch's segment)
-#ifndef YK_PRIMARY_TOUCH
-#define YK_PRIMARY_TOUCH 0
-#endif
 static_assert(kClaimTail == 0 || (kClaimTail >= 64 && kClaimTail <= YK_CLAIM), "a tail claim serves a whole wave");
-// The fused first-segment render (kMode 32): waves [0, kFusedProducers) of a
-// workgroup render first segments region by region and queue the survivors' records in LDS; the
-// others render bounces from that queue (a wave with every lane free and an empty queue renders a
-// region itself).  Producers pause while more than kQueueHi chunks wait.
-#ifndef YK_FUSED_PRODUCERS
-#define YK_FUSED_PRODUCERS 3
-#endif
-#ifndef YK_QUEUE_HI
-#define YK_QUEUE_HI 32
-#endif
-#ifndef YK_FUSED_HELP
-#define YK_FUSED_HELP 0
-#endif
-// diagnostic builds (YK_FUSED_DIAG): ykgpu_get_stats diag[0..3] = producer-wave pauses (queue
-// long), waits of waves with nothing to render, consumer trips with free lanes and no chunk,
-// regions rendered by non-producer waves
-#ifdef YK_FUSED_DIAG
-#define YK_FDIAG(k) (lane == 0 ? (void)atomicAdd(&ka.counters[19 + (k)], 1ull) : (void)0)
-#else
-#define YK_FDIAG(k) ((void)0)
-#endif
-constexpr uint32_t kFusedProducers = YK_FUSED_PRODUCERS, kQueueHi = YK_QUEUE_HI;
-// the ready queue: chunks of <= 64 continuation records (a region's survivors in kClaim / 64
-// chunks at most); every wave of a 768-thread workgroup may push a region's chunks past kQueueHi
-constexpr uint32_t kQueueCap = 128;
-static_assert(kQueueHi + (YK_BLOCK / 64) * (YK_CLAIM / 64) <= kQueueCap, "the ready queue can overflow");
-struct ReadyQueue {
-  uint32_t head, tail, producing, pad;
-  unsigned long long ent[kQueueCap];  // (first record << 32) | (count << 1) | 1; 0: not published
-};
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
@@ -236,14 +201,6 @@ struct KernelArgs {
   unsigned long long* clk;  // this launch's shader-clock probe (YK_CLOCK_*): 4 words
   // the tile's columns (include/ykgpu.h yk_render_params; the whole width: Wt = W, 0, 1, 0)
   uint32_t Wt, col_begin, col_stride, col_band;
-  // the first-segment split (yk_render_persistent kPrimary / kBounce): the paths that
-  // go on after their first segment, as continuation records compacted per 512-slot region into
-  // the start-record buffer, their (slot, seed), the regions' survivor counts, and the bounce
-  // kernel's region counter
-  uint2* meta;
-  uint32_t* rcount;
-  uint32_t* claim2;
-  uint32_t nreg, lds_queue_off;  // lds_queue_off: the fused render's ReadyQueue in LDS
 };
 
 // Shader-clock probe of a launch: thread 0 of block 0 stores s_memtime (the shader clock) and
@@ -464,7 +421,7 @@ struct WarmArgs {
   const uint32_t* order;
   uint64_t n;  // sample slots in the launch
   void* out;
-  uint32_t* counter;  // the launch's slot counters (2 words): cleared here (the render waits for this kernel)
+  uint32_t* counter;  // the launch's sample-slot counter: cleared here (the render waits for this kernel)
 };
 
 template <bool kLens, bool kF32>
@@ -472,7 +429,7 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
   // (32-bit indices: a launch keeps its slots below 2^31 and the grid below 2^21 threads)
   const uint32_t n = (uint32_t)wa.n;
   const uint32_t stride = gridDim.x * blockDim.x;
-  if (blockIdx.x == 0 && threadIdx.x < 2) wa.counter[threadIdx.x] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *wa.counter = 0u;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
     const uint32_t q = wa.order[pp];
@@ -681,186 +638,6 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
   return !in_path && slot >= ka.nsl;
 }
 
-// Refill of the bounce kernel (kBounce): lanes without a path take the next continuation records
-// of the wave's reserve; when it runs short the wave claims the next 512-slot region (one atomic),
-// whose survivors the primary kernel compacted at the region's start (rcount: how many).  A free
-// lane the reserve cannot serve this trip stays idle; it leaves the loop (returns true) once the
-// regions are exhausted.  got: this lane took record `idx`.
-__device__ __forceinline__ bool claim_regions(const KernelArgs& ka, bool in_path, uint32_t lane, uint32_t& idx,
-                                              bool& got, uint32_t& res_base, uint32_t& res_left) {
-  got = false;
-  const unsigned long long m = __ballot(!in_path);
-  if (!m) return false;
-  const uint32_t need = (uint32_t)__popcll(m);
-  uint32_t nb = 0, nleft = 0;
-  bool out = false;
-  if (res_left < need) {
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t reg = 0;
-    if ((int)lane == leader) reg = atomicAdd(ka.claim2, 1u);
-    reg = __shfl(reg, leader);
-    if (reg < ka.nreg) {
-      nb = reg * kClaim;
-      nleft = ka.rcount[reg];
-    } else {
-      out = true;
-    }
-  }
-  if (!in_path) {
-    const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (r < res_left) {
-      idx = res_base + r;
-      got = true;
-    } else if (r - res_left < nleft) {
-      idx = nb + (r - res_left);
-      got = true;
-    }
-  }
-  if (res_left < need) {
-    const uint32_t take = min(need - res_left, nleft);
-    res_base = nb + take;
-    res_left = nleft - take;
-  } else {
-    res_base += need;
-    res_left -= need;
-  }
-  return !in_path && !got && out;
-}
-
-// The fused render's ready queue (ReadyQueue, kMode 32).  Every wave of the workgroup is on this
-// CU, so workgroup-scope release / acquire order the records (global memory, this CU's L1 and its
-// XCD's L2) against the queue words in LDS.
-__device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Producer, every lane, after a region's last batch: its `count` survivors (records first ..
-// first + count - 1) as chunks of <= 64, published after the records
-__device__ __forceinline__ void queue_push(ReadyQueue* q, uint32_t first, uint32_t count, uint32_t lane) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane == 0) {
-    for (uint32_t k = 0; k < count; k += 64u) {
-      const uint32_t t = __hip_atomic_fetch_add(&q->tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const unsigned long long e =
-          ((unsigned long long)(first + k) << 32) | ((unsigned long long)min(64u, count - k) << 1) | 1ull;
-      __hip_atomic_store(&q->ent[t % kQueueCap], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __hip_atomic_fetch_sub(&q->producing, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-
-// Consumer, lane 0: the oldest published chunk, or 0 (queue empty, its head not yet published, or
-// another wave took it first)
-__device__ __forceinline__ unsigned long long queue_pop(ReadyQueue* q) {
-  const uint32_t h = lds_load(&q->head);
-  if (h == lds_load(&q->tail)) return 0;
-  const unsigned long long e = __hip_atomic_load(&q->ent[h % kQueueCap], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (!e) return 0;
-  uint32_t hx = h;
-  if (!__hip_atomic_compare_exchange_strong(&q->head, &hx, h + 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_WORKGROUP))
-    return 0;
-  __hip_atomic_store(&q->ent[h % kQueueCap], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return e;
-}
-
-// Refill of the fused render (kMode 32).  Wave-uniform state: `producing` (the wave renders the
-// first segments of region rbase .. in batches of 64 slots: every lane starts slot rbase + lane),
-// the record reserve (res_base, res_left) and pool_done (the launch's slot counter ran out).  A
-// wave that is not producing serves its free lanes from the reserve and then from the queue; one
-// with every lane free and nothing in reserve takes a region when it may (producer waves while
-// at most kQueueHi chunks wait, the others when the queue is empty).  got: this lane took record
-// `idx`.  Returns true when the wave leaves: no path, no region left and no producer that could
-// still queue one.
-__device__ __forceinline__ bool fused_refill(const KernelArgs& ka, ReadyQueue* q, bool in_path, uint32_t lane,
-                                             bool prod_role, uint32_t& idx, bool& got, bool& producing,
-                                             uint32_t& rbase, uint32_t& rleft, uint32_t& rreg, uint32_t& rrank,
-                                             uint32_t& res_base, uint32_t& res_left, bool& pool_done) {
-  got = false;
-  if (producing) {
-    idx = rbase + lane;
-    return false;
-  }
-  const unsigned long long m = __ballot(!in_path);
-  if (!m) return false;
-  if (m == ~0ull && res_left == 0 && !pool_done) {
-    uint32_t v = 0;  // 1 + the region's first slot; ~0: the slots ran out
-    if (lane == 0) {
-      const uint32_t len = lds_load(&q->tail) - lds_load(&q->head);
-      if (prod_role ? len < kQueueHi : len == 0) {
-        // counted as producing before the claim: a wave that finds the counter exhausted then
-        // also sees every region claimed before it as pushed or in progress
-        (void)__hip_atomic_fetch_add(&q->producing, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        const uint32_t fresh = atomicAdd(ka.pixel_counter, kClaim);
-        if (fresh < ka.nsl) {
-          v = fresh + 1u;
-        } else {
-          (void)__hip_atomic_fetch_sub(&q->producing, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          v = ~0u;
-        }
-      }
-    }
-    v = __shfl(v, 0);
-    if (v == ~0u) {
-      pool_done = true;
-    } else if (v) {
-      if (!prod_role) YK_FDIAG(3);
-      producing = true;
-      rbase = v - 1u;
-      rreg = rbase / kClaim;
-      rrank = 0;
-      rleft = min(kClaim, ka.nsl - rbase) / 64u;
-      idx = rbase + lane;
-      return false;
-    }
-  }
-  const uint32_t need = (uint32_t)__popcll(m);
-  uint32_t nb = 0, nleft = 0;
-  // (a producer wave takes no chunks while regions are left: it waits for the queue to shorten;
-  // YK_FUSED_HELP: it renders bounces from the queue meanwhile)
-  if (res_left < need && (YK_FUSED_HELP || !(prod_role && !pool_done))) {
-    unsigned long long e = 0;
-    if (lane == 0) e = queue_pop(q);
-    const uint32_t ehi = __shfl((uint32_t)(e >> 32), 0), elo = __shfl((uint32_t)e, 0);
-    if (elo) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the chunk's records after its entry
-      nb = ehi;
-      nleft = elo >> 1;
-    }
-  }
-  if (!in_path) {
-    const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (r < res_left) {
-      idx = res_base + r;
-      got = true;
-    } else if (r - res_left < nleft) {
-      idx = nb + (r - res_left);
-      got = true;
-    }
-  }
-  if (res_left < need) {
-    const uint32_t take = min(need - res_left, nleft);
-    res_base = nb + take;
-    res_left = nleft - take;
-  } else {
-    res_base += need;
-    res_left -= need;
-  }
-  if (__ballot(in_path || got)) {
-    if (!prod_role && res_left == 0 && __ballot(!in_path && !got)) YK_FDIAG(2);
-    return false;
-  }
-  // nothing to render this trip: leave once no chunk can come, else let the producers run
-  uint32_t done = 0;
-  if (lane == 0)
-    done = pool_done && lds_load(&q->producing) == 0 && lds_load(&q->head) == lds_load(&q->tail);
-  if (__shfl(done, 0)) return true;
-  YK_FDIAG(prod_role && !pool_done ? 0 : 1);
-  __builtin_amdgcn_s_sleep(4);
-  return false;
-}
-
 using RenderKernel = void (*)(KernelArgs);
 
 // YK_SPLIT (Makefile): 0 — every kernel in this translation unit (the A/B variants of
@@ -875,10 +652,7 @@ using RenderKernel = void (*)(KernelArgs);
 // instance carries neither their registers nor their adds)
 // kMode bit 0: the work counters; bit 1: YK_SEED_RANDOM_DEVICE seeding (an instance of its own:
 // the hash's 64-bit arithmetic and two more kernel arguments cost the counter-seeded production
-// instance 0.6% through SGPR spills); bit 2: the yk::xor128 engine (YK_RNG_XOR128); bits 3 and 4
-// (8, 16): the first-segment split's two kernels — kPrimary renders every sample's first segment in
-// coherent batches (64 consecutive slots: one 8x8 pixel block at one sample index) and hands the
-// paths that go on to kBounce, which runs the rest from those continuation records
+// instance 0.6% through SGPR spills); bit 2: the yk::xor128 engine (YK_RNG_XOR128)
 template <bool kSceneInLds, int kMode>
 __global__ __launch_bounds__(mode_block<kMode>())
 #if YK_WAVES_PER_EU
@@ -896,9 +670,6 @@ void yk_render_persistent(KernelArgs ka) {
   constexpr bool kCount = (kMode & 1) != 0;
   constexpr bool kRandomSeed = (kMode & 2) != 0;
   using Gen = typename std::conditional<(kMode & 4) != 0, ykd::X128Lane, ykd::MtLane>::type;
-  constexpr bool kPrimary = (kMode & 8) != 0, kBounce = (kMode & 16) != 0, kFused = (kMode & 32) != 0;
-  static_assert(!((kPrimary || kBounce || kFused) && ((kMode & 7) != 0)), "the split has production mt19937 instances only");
-  static_assert(!kFused || kSceneInLds, "the fused render's queue is in LDS beside the scene");
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -918,10 +689,6 @@ void yk_render_persistent(KernelArgs ka) {
     for (int k = 0; k < 5; ++k) {
       uint4* dst = (uint4*)(smem + off[k]);
       for (uint32_t i = threadIdx.x; i < n16[k]; i += kBlk) dst[i] = src[k][i];
-    }
-    if constexpr (kFused) {
-      uint32_t* const qw = (uint32_t*)(smem + ka.lds_queue_off);
-      for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(ReadyQueue) / 4); i += kBlk) qw[i] = 0;
     }
     __syncthreads();
     nodes = smem;
@@ -958,48 +725,10 @@ void yk_render_persistent(KernelArgs ka) {
   bool in_path = false;
   // wave-level reserve of claimed sample slots (identical in every lane of the wave)
   uint32_t res_base = 0, res_left = 0;
-  // kPrimary: the wave's region (512 slots = 8 batches of 64), the batches left in it and the
-  // survivors compacted so far (wave-uniform)
-  uint32_t rbase = 0, rleft = 0, rreg = 0, rrank = 0;
-  bool got = false;  // kBounce: this lane took a continuation record this trip
-  // kFused: this wave renders a region's first segments now (wave-uniform); the launch's slots ran
-  // out; the wave is one of the workgroup's producers; the ready queue
-  bool producing = false, pool_done = false;
-  const bool prod_role = (threadIdx.x >> 6) < kFusedProducers;
-  ReadyQueue* const rq = (ReadyQueue*)(smem + ka.lds_queue_off);
-#if YK_PRIMARY_TOUCH
-  uint32_t touch = 0;
-#endif
 
   for (;;) {
     // ---- refill (claim_slots): lanes without a path take the next sample slots
-    if constexpr (kPrimary) {
-      // a batch: every lane starts slot rbase + lane (every lane's previous path has ended or
-      // been handed over)
-      if (rleft == 0) {
-        uint32_t fresh = 0;
-        if (lane == 0) fresh = atomicAdd(ka.pixel_counter, kClaim);
-        fresh = __shfl(fresh, 0);
-        if (fresh >= ka.nsl) break;
-        rbase = fresh;
-        rreg = fresh / kClaim;
-        rrank = 0;
-        rleft = min(kClaim, ka.nsl - fresh) / 64u;
-      }
-      slot = rbase + lane;
-#if YK_PRIMARY_TOUCH
-      // the next batch's start records, touched now: their latency passes under this batch's
-      // segment (the value is consumed after the segment, so the wait for it lands there), and
-      // the next batch's loads find them in the cache
-      touch = rleft > 1 ? *((const volatile uint32_t*)ka.start + 16u * (slot + 64u)) : 0u;
-#endif
-    } else if constexpr (kBounce) {
-      if (claim_regions(ka, in_path, lane, slot, got, res_base, res_left)) break;
-    } else if constexpr (kFused) {
-      if (fused_refill(ka, rq, in_path, lane, prod_role, slot, got, producing, rbase, rleft, rreg, rrank, res_base,
-                       res_left, pool_done))
-        break;
-    } else if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) {
+    if (claim_slots(ka, in_path, lane, slot, res_base, res_left)) {
       YK_STAMPS_EXHAUSTED(ka.counters);
       break;
     }
@@ -1013,24 +742,7 @@ void yk_render_persistent(KernelArgs ka) {
     // record's j, then its other words under the test).  Every slot of the launch, padded ones
     // included, has a record, so the read is in bounds.
     uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0}, rq3 = {0, 0, 0, 0};
-    uint2 meta = {0, 0};
-    // the wave renders bounces from continuation records (kBounce; kFused when not producing)
-    const bool from_rec = kBounce || (kFused && !producing);
-    if (from_rec) {
-      // a continuation record (compacted index `slot`) and its (slot, seed), loaded together
-      start = start && got;
-      if (start) {
-        const uint4* rp = (const uint4*)ka.start + 4u * slot;
-        rq0 = rp[0];
-        rq1 = rp[1];
-        rq2 = rp[2];
-        rq3 = rp[3];
-        meta = ka.meta[slot];
-        asm volatile("" ::"v"(rq0.x), "v"(rq0.y), "v"(rq0.z), "v"(rq0.w), "v"(rq1.x), "v"(rq1.y),
-                     "v"(rq1.z), "v"(rq1.w), "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(rq3.x),
-                     "v"(rq3.y), "v"(rq3.z), "v"(rq3.w), "v"(meta.x), "v"(meta.y));
-      }
-    } else if (start) {
+    if (start) {
       const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
       qpix = ka.order[slot - sl * ka.npix_slots];
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
@@ -1045,37 +757,6 @@ void yk_render_persistent(KernelArgs ka) {
       }
       start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
-    if constexpr (kBounce || kFused) if (from_rec) {
-      if (start) {
-        slot = meta.x;
-        StartRec r;
-        __builtin_memcpy((char*)&r, &rq0, 16);
-        __builtin_memcpy((char*)&r + 16, &rq1, 16);
-        __builtin_memcpy((char*)&r + 32, &rq2, 16);
-        __builtin_memcpy((char*)&r + 48, &rq3, 16);
-        if (r.j != kNoStart) {
-          // the engine, the scattered ray and the attenuation stack after the first segment
-          // (the primary kernel's hand-over: j | nstk << 8 | newest id << 16)
-          g.seed = meta.y;
-          g.a0 = r.a0;
-          g.a1 = r.a1;
-          g.b = r.b;
-          g.j = r.j & 0xffu;
-          o = v3{r.ox, r.oy, r.oz};
-          d = v3{r.dx, r.dy, r.dz};
-          nstk = (r.j >> 8) & 1u;
-          st0 = r.j >> 16;
-          st1 = st2 = st3 = 0;
-          depth = ka.max_depth - 1u;
-          in_path = true;
-          start = false;
-        } else {
-          // the primary kernel's lane reached the scratch engine: the whole sample again
-          const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
-          qpix = ka.order[slot - sl * ka.npix_slots];
-        }
-      }
-    }
     if (start) {
       // The start — the jitter canonicals, the lens point and the camera ray — and the engine
       // after its draws: precomputed for mt19937 by yk_mt_warmup (StartRec), so the divergent
@@ -1089,23 +770,21 @@ void yk_render_persistent(KernelArgs ka) {
       const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
       bool pre = false;
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
-        if (!from_rec) {
-          StartRec r;  // (loaded above with the pixel)
-          __builtin_memcpy((char*)&r, &rq0, 16);
-          __builtin_memcpy((char*)&r + 16, &rq1, 16);
-          __builtin_memcpy((char*)&r + 32, &rq2, 16);
-          __builtin_memcpy((char*)&r + 48, &rq3, 16);
-          pre = r.j != kNoStart;
-          if (pre) {
-            if (kCount) n_swords += r.j;
-            g.seed = seed;  // (the scratch engine's seeding needs it)
-            g.a0 = r.a0;
-            g.a1 = r.a1;
-            g.b = r.b;
-            g.j = r.j;
-            o = v3{r.ox, r.oy, r.oz};
-            d = v3{r.dx, r.dy, r.dz};
-          }
+        StartRec r;  // (loaded above with the pixel)
+        __builtin_memcpy((char*)&r, &rq0, 16);
+        __builtin_memcpy((char*)&r + 16, &rq1, 16);
+        __builtin_memcpy((char*)&r + 32, &rq2, 16);
+        __builtin_memcpy((char*)&r + 48, &rq3, 16);
+        pre = r.j != kNoStart;
+        if (pre) {
+          if (kCount) n_swords += r.j;
+          g.seed = seed;  // (the scratch engine's seeding needs it)
+          g.a0 = r.a0;
+          g.a1 = r.a1;
+          g.b = r.b;
+          g.j = r.j;
+          o = v3{r.ox, r.oy, r.oz};
+          d = v3{r.dx, r.dy, r.dz};
         }
       }
       if (!pre) {
@@ -1502,39 +1181,6 @@ void yk_render_persistent(KernelArgs ka) {
     }
     YK_STAMP(4);
 
-    if constexpr (kPrimary || kFused) if (kPrimary || producing) {
-#if YK_PRIMARY_TOUCH
-      asm volatile("" ::"v"(touch));
-#endif
-      // hand the paths that go on to the bounce kernel: a continuation record over a start
-      // record this wave has already read (compacted at its region's start: index < this batch's
-      // end) and the sample's (slot, seed); a path that reached the scratch engine (per-lane
-      // state that cannot move) is handed over as a restart (j = kNoStart)
-      const bool hand = in_path && !ended;
-      const unsigned long long hm = __ballot(hand);
-      if (hand) {
-        const uint32_t idx = rreg * kClaim + rrank + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
-        const uint32_t pk = ykd::mt_used_fallback(g) ? kNoStart : (g.j | (nstk << 8) | (st0 << 16));
-        uint4* const rp = (uint4*)ka.start + 4u * idx;
-        *(double2*)rp = make_double2(o.x, o.y);
-        *(double2*)(rp + 1) = make_double2(o.z, d.x);
-        *(double2*)(rp + 2) = make_double2(d.y, d.z);
-        rp[3] = make_uint4(g.a0, g.a1, g.b, pk);
-        ka.meta[idx] = make_uint2(slot, g.seed);
-        in_path = false;
-      }
-      rrank += (uint32_t)__popcll(hm);
-      rbase += 64u;
-      if (--rleft == 0) {
-        if constexpr (kFused) {
-          queue_push(rq, rreg * kClaim, rrank, lane);
-          producing = false;
-        } else if (lane == 0) {
-          ka.rcount[rreg] = rrank;
-        }
-      }
-    }
-
     if (ended) {
       // unwind: attenuation_k * (...) from the deepest scatter outwards (raytracer.hpp:31)
       auto pop = [&]() {
@@ -1594,13 +1240,6 @@ RenderKernel fp64_kernel(bool lds, int mode) {
       yk_render_persistent<true, 7>};
   return k[(lds ? 8 : 0) + (mode & 7)];
 }
-// The first-segment split's kernels (production FP64 mt19937, scene in LDS): the coherent first
-// segments (kPrimary) and the bounces after them (kBounce)
-RenderKernel split_kernel(bool bounce) {
-  return bounce ? yk_render_persistent<true, 16> : yk_render_persistent<true, 8>;
-}
-// ... and the fused render: both in one kernel, the hand-over through the workgroup's LDS queue
-RenderKernel fused_kernel() { return yk_render_persistent<true, 32>; }
 
 #endif  // YK_SPLIT != 2
 
@@ -2270,9 +1909,6 @@ struct ykgpu_context {
   size_t scratch_lanes = 0;
   char* d_warm = nullptr;  // warm-up ring: a StartRec (FP64) or StartRecF (FP32) per sample slot
   double* d_col = nullptr;     // sample colours of one launch (kColStride doubles per slot)
-  uint2* d_meta = nullptr;     // first-segment split: (slot, seed) per continuation record, warm ring
-  uint32_t* d_rcount = nullptr;  // ... and survivors per 512-slot region
-  size_t meta_cap = 0, rcount_cap = 0;
   double* d_acc = nullptr;     // running per-pixel sums between launches
   size_t col_cap = 0, acc_cap = 0;
   uint32_t* d_order = nullptr;  // processing slot → tile pixel, for (order_w, order_rows)
@@ -2295,12 +1931,11 @@ struct ykgpu_context {
   // equal (launch() `ov`; equal slot offsets in every ring buffer and scratch slice)
   struct RingGeom {
     uint64_t nps = 0, K = 0, welem = 0, warm_ring = 0, col_ring = 0, lanes = 0, id_stride = 0;
-    const void *warm = nullptr, *col = nullptr, *mt = nullptr, *ids = nullptr, *meta = nullptr, *rcount = nullptr;
-    bool split = false;
+    const void *warm = nullptr, *col = nullptr, *mt = nullptr, *ids = nullptr;
     bool operator==(const RingGeom& o) const {
       return nps == o.nps && K == o.K && welem == o.welem && warm_ring == o.warm_ring && col_ring == o.col_ring &&
              lanes == o.lanes && id_stride == o.id_stride && warm == o.warm && col == o.col && mt == o.mt &&
-             ids == o.ids && meta == o.meta && rcount == o.rcount && split == o.split;
+             ids == o.ids;
     }
   } prev_geom;
   uint64_t prev_shape = 0;  // (nps, kmax, precision, engine) of the previous call: launch() `inflight`
@@ -2471,14 +2106,6 @@ constexpr uint32_t kLaunchesPerCall = YK_LAUNCHES_PER_CALL;
 #define YK_LAUNCH_SLOTS (1u << 25)
 #endif
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
-// The first-segment split: FP64 mt19937 production renders with the scene in LDS run
-// every sample's first segment in coherent batches (kPrimary) and the rest from continuation
-// records (kBounce); 2: both in one kernel, the hand-over through an LDS queue per workgroup
-// (kFused); 0: one persistent kernel for the whole path, as before round 5
-#ifndef YK_PRIMARY_SPLIT
-#define YK_PRIMARY_SPLIT 0
-#endif
-constexpr bool kPrimarySplit = YK_PRIMARY_SPLIT != 0, kPrimaryFused = YK_PRIMARY_SPLIT == 2;
 // Under memory pressure (launch()): launches shrink down to this many sample slots before a call
 // fails with YK_ERR_NOMEM, and the rings leave kMemReserve of the device free
 constexpr uint64_t kMemFloorSlots = 1ull << 24;
@@ -2569,11 +2196,6 @@ int ensure_order(ykgpu_context* ctx, uint32_t W, uint32_t rows, uint32_t stride)
 // Render streams get the device's top priority (YKGPU_RENDER_PRIO=0: default priority, A/B): when
 // a launch drains, the queued warm-up and reduce blocks would otherwise take the CUs it frees
 // before the next launch's workgroups (one per CU, 768 threads and most of the LDS) fit.
-// the reduce stream at the render streams' priority (A/B: a reduce that shares the CUs with a
-// warm-up's grid can take several times its ~0.9 ms, and render c + 2 waits for it)
-#ifndef YK_REDUCE_PRIO
-#define YK_REDUCE_PRIO 0
-#endif
 hipError_t create_render_stream(hipStream_t* s) {
   int least = 0, greatest = 0;
   const char* e = ab_knob("YKGPU_RENDER_PRIO");
@@ -2771,20 +2393,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     break;
   }
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
-  // the first-segment split: its hand-over records live in the start-record ring; per ring buffer
-  // the records' (slot, seed) and every 512-slot region's survivor count
-  const bool split = kPrimarySplit && !f32 && !x128 && plan.in_lds && !warm_first &&
-                     !(p->flags & (YK_FLAG_COUNT_WORK | YK_FLAG_TRACE_RAYS | YK_FLAG_ONE_LANE)) &&
-                     p->seed_mode == YK_SEED_COUNTER && p->max_depth >= 1;
-  const size_t nreg_max = ((size_t)nps * K + kClaim - 1) / kClaim;
-  // the fused render's queue goes after the stacks (when the CU's LDS has room for it)
-  const uint32_t queue_off = (plan.lds_bytes + 15u) & ~15u;
-  const bool fused = split && kPrimaryFused && queue_off + sizeof(ReadyQueue) <= 160u * 1024u;
-  if (split) {
-    if ((rc = grow(ctx->d_meta, ctx->meta_cap, (size_t)kWarmRing * nps * K, sizeof(uint2)))) return rc;
-    if (!fused && (rc = grow(ctx->d_rcount, ctx->rcount_cap, (size_t)kWarmRing * nreg_max, sizeof(uint32_t))))
-      return rc;
-  }
   KernelArgs ka;
   ka.cam = ctx->cam;
   ka.pad_a = 0;
@@ -2844,10 +2452,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.seed_mode = p->seed_mode;
   ka.seed_key = seed_key;
   ka.pixel_counter = ctx->d_counter;
-  ka.meta = nullptr;
-  ka.rcount = nullptr;
-  ka.claim2 = nullptr;
-  ka.nreg = ka.lds_queue_off = 0;
 
   ka.counters = ctx->d_stats;
   ka.trace = ctx->d_trace;
@@ -2922,9 +2526,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   geom.col = ctx->d_col;
   geom.mt = ctx->d_mt;
   geom.ids = ctx->d_ids;
-  geom.split = split;
-  geom.meta = split ? ctx->d_meta : nullptr;
-  geom.rcount = split ? ctx->d_rcount : nullptr;
   const char* ove = std::getenv("YKGPU_OVERLAP");
   const bool ov = !x128 && !warm_first && !(ove && std::atoi(ove) == 0) && ctx->prev_ok && ctx->prev_geom == geom &&
                   ctx->prev_n >= std::max(kWarmRing, kColRing);
@@ -2943,8 +2544,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     ctx->d_counter = nullptr;
     ctx->d_clk = nullptr;
     ctx->counter_cap = 0;
-    // two words per start-record buffer (the slot counter; the split's bounce-region counter)
-    YK_HIP(hipMalloc(&ctx->d_counter, 2ull * std::max(nlaunch, kWarmRing) * sizeof(uint32_t)));
+    YK_HIP(hipMalloc(&ctx->d_counter, std::max(nlaunch, kWarmRing) * sizeof(uint32_t)));
     YK_HIP(hipMalloc(&ctx->d_clk, 4ull * std::max(nlaunch, kWarmRing) * sizeof(unsigned long long)));
     ctx->counter_cap = std::max(nlaunch, kWarmRing);
   }
@@ -2990,7 +2590,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     wa.s0 = sched[c].first;
     wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)((g0 + c) % kWarmRing) * nps * K * welem;
-    wa.counter = ctx->d_counter + 2 * ((g0 + c) % kWarmRing);
+    wa.counter = ctx->d_counter + (g0 + c) % kWarmRing;
     const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * warm_per_cu(f32));
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
@@ -3035,26 +2635,11 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));
     else if (ov)
       YK_HIP(hipStreamWaitEvent(rs, ctx->lev_prev[6 * (pn - kColRing + c) + 5], 0));
-    ka.pixel_counter = ctx->d_counter + (x128 ? c : 2u * (uint32_t)(g % kWarmRing));
-    ka.claim2 = ka.pixel_counter + 1;
+    ka.pixel_counter = ctx->d_counter + (x128 ? c : (uint32_t)(g % kWarmRing));
     ka.clk = ctx->d_clk + 4 * c;
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
-    if (split) {
-      // every sample's first segment in coherent batches, then the rest from its hand-over records,
-      // on the same stream (the bounce kernel reads what the primary kernel wrote)
-      ka.meta = ctx->d_meta + (size_t)(g % kWarmRing) * nps * K;
-      if (fused) {
-        ka.lds_queue_off = queue_off;
-        hipLaunchKernelGGL(fused_kernel(), dim3(grid), dim3(block), queue_off + sizeof(ReadyQueue), rs, ka);
-      } else {
-        ka.rcount = ctx->d_rcount + (size_t)(g % kWarmRing) * nreg_max;
-        ka.nreg = (uint32_t)(((uint64_t)nsl + kClaim - 1) / kClaim);
-        hipLaunchKernelGGL(split_kernel(false), dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
-        YK_HIP(hipGetLastError());
-        hipLaunchKernelGGL(split_kernel(true), dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
-      }
-    } else if (f32)
+    if (f32)
       hipLaunchKernelGGL(f32_kernel(plan.in_lds, (count ? 1 : 0) | (x128 ? 4 : 0)), dim3(grid), dim3(block),
                          plan.lds_bytes, rs, ka);
     else
@@ -3100,8 +2685,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
                   (uint64_t)ctx->nspheres * (sizeof(SphereGeo) + sizeof(SphereMat) + sizeof(float4));
     cb += (uint64_t)kColRing * nps * K * kColStride * sizeof(double) + (x128 ? 0 : (uint64_t)kWarmRing * nps * K * welem);
     cb += (nlaunch > 1 ? (uint64_t)nps * 3 * sizeof(double) : 0) + (uint64_t)nps * sizeof(uint32_t);
-    cb += 2ull * nlaunch * sizeof(uint32_t) + kCounters * sizeof(unsigned long long);
-    if (split) cb += (uint64_t)kWarmRing * nps * K * sizeof(uint2) + (fused ? 0 : kWarmRing * nreg_max * sizeof(uint32_t));
+    cb += nlaunch * sizeof(uint32_t) + kCounters * sizeof(unsigned long long);
     if (!x128) cb += 2 * lanes * ykd::kMtN * sizeof(uint32_t);
     cb += 2 * lanes * std::max(1u, p->max_depth > kStackRegs ? p->max_depth : 1u) * sizeof(uint16_t);
     const uint64_t npix = (uint64_t)p->row_count * tile_width(p);
@@ -3117,8 +2701,7 @@ uint64_t device_bytes(const ykgpu_context* ctx) {
   uint64_t b = ctx->t64.bytes + ctx->t32.bytes;
   if (ctx->d_geo) b += (uint64_t)ctx->nspheres * (sizeof(SphereGeo) + sizeof(SphereMat) + sizeof(float4));
   b += ctx->warm_cap + ctx->col_cap * sizeof(double) + ctx->acc_cap * sizeof(double);
-  b += ctx->meta_cap * sizeof(uint2) + ctx->rcount_cap * sizeof(uint32_t);
-  b += (uint64_t)ctx->order_slots * sizeof(uint32_t) + 2ull * ctx->counter_cap * sizeof(uint32_t);
+  b += (uint64_t)ctx->order_slots * sizeof(uint32_t) + (uint64_t)ctx->counter_cap * sizeof(uint32_t);
   b += kCounters * sizeof(unsigned long long);
   if (ctx->d_mt) b += 2ull * ctx->scratch_lanes * ykd::kMtN * sizeof(uint32_t);
   if (ctx->d_ids) b += 2ull * ctx->id_lanes * ctx->id_stride * sizeof(uint16_t);
@@ -3317,14 +2900,9 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
   for (int k8 = 0; k8 < 8; ++k8)
     (void)hipFuncSetAttribute((const void*)f32_kernel(k8 & 4, (k8 & 1) | ((k8 & 2) << 1)),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  for (bool bounce : {false, true})
-    (void)hipFuncSetAttribute((const void*)split_kernel(bounce), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-  (void)hipFuncSetAttribute((const void*)fused_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
-      (YK_REDUCE_PRIO ? create_render_stream(&ctx->red) : hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking)) !=
-          hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
       create_render_stream(&ctx->alt) != hipSuccess || create_render_stream(&ctx->ren) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
@@ -3349,8 +2927,6 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_order);
   (void)hipFree(ctx->d_col);
   (void)hipFree(ctx->d_acc);
-  (void)hipFree(ctx->d_meta);
-  (void)hipFree(ctx->d_rcount);
   ctx->t64.release();
   ctx->t32.release();
   (void)hipFree(ctx->d_mt);
