@@ -152,6 +152,9 @@ constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
 #endif
 constexpr uint32_t kClaimTail = YK_CLAIM_TAIL, kClaimTailFactor = YK_CLAIM_TAIL_FACTOR;
 static_assert(kClaimTail == 0 || (kClaimTail >= 64 && kClaimTail <= YK_CLAIM), "a tail claim serves a whole wave");
+#ifndef YK_WG_HOLD
+#define YK_WG_HOLD 0
+#endif
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
@@ -201,6 +204,9 @@ struct KernelArgs {
   unsigned long long* clk;  // this launch's shader-clock probe (YK_CLOCK_*): 4 words
   // the tile's columns (include/ykgpu.h yk_render_params; the whole width: Wt = W, 0, 1, 0)
   uint32_t Wt, col_begin, col_stride, col_band;
+#ifdef YK_DRAIN_DIAG
+  uint32_t diag_c, diag_pad;  // the launch's index in its call
+#endif
 };
 
 // Shader-clock probe of a launch: thread 0 of block 0 stores s_memtime (the shader clock) and
@@ -216,6 +222,30 @@ struct KernelArgs {
   } while (0)
 #define YK_CLOCK_BEGIN(ka) YK_CLOCK_STAMP(ka, 0)
 #define YK_CLOCK_END(ka) YK_CLOCK_STAMP(ka, 2)
+
+// Diagnostic builds (YK_DRAIN_DIAG, tools/drain_probe.py): every FP64 render wave records when it
+// starts and when it leaves the loop (s_memrealtime, 100 MHz) and where it ran (HW_ID, XCC_ID), per
+// launch of the call: the per-launch drain — waves idle in a workgroup that still holds its CU,
+// CUs between one launch's workgroup and the next — measured, not modelled
+#ifdef YK_DRAIN_DIAG
+constexpr uint32_t kDiagLaunches = 64, kDiagBlocks = 512, kDiagWaves = 16;
+// per wave: {start, end, HW_ID | XCC_ID << 32}
+__device__ unsigned long long yk_wave_times[kDiagLaunches * kDiagBlocks * kDiagWaves * 3];
+#define YK_WAVE_STAMP(ka, k)                                                                          \
+  do {                                                                                                \
+    const uint32_t w_ = threadIdx.x >> 6;                                                             \
+    if ((threadIdx.x & 63u) == 0 && (ka).diag_c < kDiagLaunches && blockIdx.x < kDiagBlocks) {        \
+      unsigned long long* r_ =                                                                        \
+          yk_wave_times + (((size_t)(ka).diag_c * kDiagBlocks + blockIdx.x) * kDiagWaves + w_) * 3;     \
+      r_[(k)] = __builtin_amdgcn_s_memrealtime();                                                     \
+      if ((k) == 0)                                                                                   \
+        r_[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                       \
+                ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32);                \
+    }                                                                                                 \
+  } while (0)
+#else
+#define YK_WAVE_STAMP(ka, k) ((void)0)
+#endif
 
 // -l 3 (raytracer.hpp:21-25): ray k of the path of the lane's sample slot (counting instance)
 template <class V>
@@ -707,6 +737,7 @@ void yk_render_persistent(KernelArgs ka) {
   __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);
 #endif
   YK_CLOCK_BEGIN(ka);
+  YK_WAVE_STAMP(ka, 0);
 
   Gen g;
   rng_init(g, ka, gid);
@@ -1208,6 +1239,7 @@ void yk_render_persistent(KernelArgs ka) {
   }
 
   YK_CLOCK_END(ka);
+  YK_WAVE_STAMP(ka, 1);
   YK_STAMPS_END(ka.counters, lane);
   if (kCount) {
     atomicAdd(&ka.counters[0], (unsigned long long)n_seg);
@@ -1227,6 +1259,12 @@ void yk_render_persistent(KernelArgs ka) {
     atomicAdd(&ka.counters[31], (unsigned long long)n_twist);
   }
   if (n_fb) atomicAdd(&ka.counters[3], (unsigned long long)n_fb);
+#if YK_WG_HOLD
+  // (A/B) the workgroup's waves leave together: a wave without work keeps its registers until the
+  // last one is done, so the CU frees whole and the next launch's workgroup is not starved by the
+  // warm-up's small workgroups taking the registers piecemeal
+  if constexpr (kMode == 0) __syncthreads();
+#endif
 }
 
 // The FP64 instance for (scene in LDS, kMode)
@@ -2232,8 +2270,16 @@ uint32_t reduce_blocks(const ykgpu_context* ctx, uint32_t nps) {
 // path and takes every idle issue slot it can (32; 16: neutral, 8: +1.8%); the FP32 one has
 // slack, and each resident warm-up wave delays the latency-bound render waves it shares a SIMD
 // with (512-spp FP32 A/B: 32 -> 205.2 ms, 4 -> 202.4, 3 -> 202.4, 2 -> 201.3)
+// FP64 warm-up grid: blocks per CU (each thread walks n / grid slots, at least kWarmSlots)
+#ifndef YK_WARM_PER_CU
+#define YK_WARM_PER_CU 32
+#endif
+#ifndef YK_WARM_SLOTS
+#define YK_WARM_SLOTS 4
+#endif
+constexpr uint32_t kWarmSlots = YK_WARM_SLOTS;
 uint32_t warm_per_cu(bool f32) {
-  uint32_t per_cu = f32 ? 2u : 32u;
+  uint32_t per_cu = f32 ? 2u : (uint32_t)YK_WARM_PER_CU;
   if (const char* e = ab_knob("YKGPU_WARM_PER_CU")) per_cu = (uint32_t)std::max(1, std::atoi(e));
   return per_cu;
 }
@@ -2591,7 +2637,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)((g0 + c) % kWarmRing) * nps * K * welem;
     wa.counter = ctx->d_counter + (g0 + c) % kWarmRing;
-    const uint32_t wblocks = (uint32_t)std::min<uint64_t>((wa.n + 1023) / 1024, (uint64_t)ctx->cus * warm_per_cu(f32));
+    const uint32_t wblocks =
+        (uint32_t)std::min<uint64_t>((wa.n + 256 * kWarmSlots - 1) / (256 * kWarmSlots), (uint64_t)ctx->cus * warm_per_cu(f32));
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
       if (f32 && wa.lens)
@@ -2637,6 +2684,10 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       YK_HIP(hipStreamWaitEvent(rs, ctx->lev_prev[6 * (pn - kColRing + c) + 5], 0));
     ka.pixel_counter = ctx->d_counter + (x128 ? c : (uint32_t)(g % kWarmRing));
     ka.clk = ctx->d_clk + 4 * c;
+#ifdef YK_DRAIN_DIAG
+    ka.diag_c = c;
+    ka.diag_pad = 0;
+#endif
     YK_HIP(hipEventRecord(ev[2], rs));
     const bool count = (ka.flags & YK_FLAG_COUNT_WORK) != 0;
     if (f32)
@@ -2864,6 +2915,23 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
 extern "C" {
 
 uint32_t ykgpu_abi_version(void) { return YKGPU_ABI_VERSION; }
+
+#ifdef YK_DRAIN_DIAG
+// (diagnostic builds only, tools/drain_probe.py) the wave records since the last clear:
+// [launch][block][wave] x {start, end, HW_ID | XCC_ID << 32}
+int ykgpu_diag_wave_times(unsigned long long* out, size_t n) {
+  const size_t cap = sizeof(yk_wave_times) / sizeof(unsigned long long);
+  YK_HIP(hipDeviceSynchronize());
+  YK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(yk_wave_times), std::min(n, cap) * sizeof(unsigned long long)));
+  return YK_OK;
+}
+int ykgpu_diag_wave_times_clear(void) {
+  YK_HIP(hipDeviceSynchronize());
+  static std::vector<unsigned long long> z(sizeof(yk_wave_times) / sizeof(unsigned long long), 0ull);
+  YK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(yk_wave_times), z.data(), z.size() * sizeof(unsigned long long)));
+  return YK_OK;
+}
+#endif
 
 const char* ykgpu_last_error(void) { return g_last_error.c_str(); }
 
