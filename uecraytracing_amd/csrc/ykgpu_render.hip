@@ -470,6 +470,15 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
     const uint32_t seed = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
     uint32_t x[1] = {seed};
     ykd::mt_walk397xn<1>(x);
+#ifdef YK_WALK_SENS
+    // (sensitivity probe, never in the product: YK_WALK_SENS more walks of a perturbed seed, their
+    // result folded in as a no-op the compiler cannot prove)
+    for (int r_ = 0; r_ < YK_WALK_SENS; ++r_) {
+      uint32_t z[1] = {seed ^ (0x9e3779b9u + (uint32_t)r_)};
+      ykd::mt_walk397xn<1>(z);
+      x[0] ^= (z[0] == 0x12345678u && seed == 0x9abcdef0u) ? 1u : 0u;
+    }
+#endif
     ykd::MtLane g;
     g.state = nullptr;
     ykd::mt_start_from(g, seed, x[0]);
