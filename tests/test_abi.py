@@ -32,6 +32,16 @@ def test_library_exports_every_declared_symbol():
     assert lib.ykgpu_abi_version() == yk.ABI_VERSION == 11
 
 
+def test_library_carries_no_diagnostic_entry_points():
+    """The per-wave drain stamps (-DYK_DRAIN_DIAG, tools/drain_probe.py) are a diagnostic build's:
+    the product library exports none of their accessors and holds no stamp buffer."""
+    lib = yk.load_library()
+    for name in ("ykgpu_diag_wave_times", "ykgpu_diag_wave_times_clear"):
+        assert not hasattr(lib, name), name
+    blob = open(yk.LIB_PATH, "rb").read()
+    assert b"yk_wave_times" not in blob
+
+
 def test_reference_camera_matches_camera_hpp():
     assert yk.reference_camera().as_tuple() == refscenes.reference_camera().as_tuple()
 
