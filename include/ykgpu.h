@@ -198,12 +198,13 @@ typedef struct yk_render_stats {
                               the full mt19937 state (samples past 227 words)            */
   uint64_t device_bytes;   /* device memory the context holds after the call: scene, BVHs,
                               processing order, start-record (xor128: colour) ring, running
-                              sums, MT and attenuation scratch, output buffers.
+                              sums, MT and attenuation scratch, the warm-ups' lens-retry rings,
+                              output buffers.
                               Buffers follow the calls: grown when a call needs more, given
                               back when it needs less than half                            */
   uint64_t call_bytes;     /* device memory THIS call needed (the same items sized to it):
-                              1920x1080x512 FP64 ~18.1 GB; the 8-GPU split's tile of 3840x2160x1024
-                              (480 columns) ~9.8 GB; 1920x1080x4096 (config 5) ~69 GB       */
+                              1920x1080x512 FP64 ~19.1 GB; the 8-GPU split's tile of 3840x2160x1024
+                              (480 columns) ~10.4 GB; 1920x1080x4096 (config 5) ~71 GB      */
   double sclk_mhz;         /* the shader clock the render launches ran at: s_memtime over
                               s_memrealtime (100 MHz) of one wave per launch, averaged      */
   uint32_t launch_spp;     /* samples per pixel of the call's largest launch (ABI 11)        */

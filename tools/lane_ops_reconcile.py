@@ -17,11 +17,19 @@ the same samples.  Per kernel:
   the two calls' wave-instruction counts (SQ_INSTS_VALU, same samples and lane masks) carries the
   one-lane count over to it, and call A's PMC figure checks that within 10%.  (The counters' own
   adds, one per counted event, are only part of the difference: counting_increments_per_sample.)
-* yk_mt_warmup — the model is the kernel's instruction count per sample read off its ISA
-  (yk_mt_warmup<true, false>, hipcc --cuda-device-only -S; tools/lane_ops_reconcile.py WARM_*):
-  the index math and seed (31 VALU), the walk loop (12 VALU per 4 steps, 99 trips), the rest of
-  the start's draws and the camera ray (146), and 108 per thin-lens rejection iteration (4 words
-  each: the iterations are (start words - 4) / 4 per sample, from the work counters).
+* the warm-up — the model is the kernel's instruction count per sample read off its ISA
+  (hipcc --cuda-device-only -S, VALU per basic block), times the lanes that run each block:
+  - yk_mt_warmup<true, false> (the rejection loop in line, WARM_*): the index math and seed (31
+    VALU), the walk loop (12 VALU per 4 steps, 99 trips), the rest of the start's draws and the
+    camera ray (146), and 108 per thin-lens rejection iteration (4 words each: the iterations are
+    (start words - 4) / 4 per sample, from the work counters);
+  - yk_mt_warmup_defer (the retries drawn after the walks, DEFER_*; round 5's production warm-up
+    for launches of <= 4096 slots per wave): per sample the loop body through the first
+    candidate (1424: index math, seed, walk, the start's draws, the candidate, the latch), then
+    the camera ray and StartRec (48) for a sample accepted there or the ring store (10) for one
+    rejected; per retry the ring read and the candidate (7 + 9 + 106), then the ring store (9) or
+    the camera ray (71).  Rejections at the first candidate are taken at their expectation
+    (1 - pi/4 per sample); every retry ends a rejection, so retries = candidates - samples.
 * The algorithmic lane-ops (uecraytracing_amd/flops.py lane_ops) over the executed ones: how much
   of what the VALU executes is the reference's own arithmetic.
 """
@@ -42,8 +50,15 @@ WARM_FIXED = 26 + 5 + 31 + 115
 WARM_WALK_LOOP = 12 * 99
 WARM_LENS_ITER = 108
 
+# yk_mt_warmup_defer (ISA of the round-5 build: VALU per basic block, see the docstring)
+DEFER_MAIN = 23 + 3 + 5 + 12 * 99 + 200 + 3 + 2
+DEFER_FINISH_MAIN, DEFER_PUT_MAIN = 48, 10
+DEFER_RETRY = 7 + 9 + 106
+DEFER_PUT_RETRY, DEFER_FINISH_RETRY = 9, 71
+P_REJECT = 1.0 - 3.141592653589793 / 4.0
+
 RENDER = "yk_render_persistent<true, "
-WARM = "yk_mt_warmup<true, false>"
+WARM = "yk_mt_warmup"  # yk_mt_warmup<true, false> or yk_mt_warmup_defer
 
 
 def dispatches(pmc_dir):
@@ -108,8 +123,15 @@ def main():
     alg_r = sum(lo["render"].values())
     alg_w = sum(lo["warmup"].values())
     swords = st["work"][6]
-    lens_iters = max(0.0, (swords - 4.0 * n) / 4.0)
-    warm_model = n * (WARM_FIXED + WARM_WALK_LOOP) + lens_iters * WARM_LENS_ITER
+    lens_iters = max(0.0, (swords - 4.0 * n) / 4.0)  # thin-lens candidates per sample x samples
+    defer = any("yk_mt_warmup_defer" in d["kernel"] for d in disp.values())
+    if defer:
+        rej1 = P_REJECT * n
+        retries = max(0.0, lens_iters - n)
+        warm_model = (n * DEFER_MAIN + (n - rej1) * DEFER_FINISH_MAIN + rej1 * DEFER_PUT_MAIN
+                      + retries * DEFER_RETRY + (retries - rej1) * DEFER_PUT_RETRY + rej1 * DEFER_FINISH_RETRY)
+    else:
+        warm_model = n * (WARM_FIXED + WARM_WALK_LOOP) + lens_iters * WARM_LENS_ITER
     e_w, lu_w = executed(wa)
     res = {
         "workload": pr["workload"], "samples": n, "images_equal": pr["images_equal"],
@@ -134,6 +156,7 @@ def main():
             "model_isa_lane_ops_per_sample": round(warm_model / n, 2),
             "model_over_pmc": round(warm_model / e_w, 4),
             "lens_iterations_per_sample": round(lens_iters / n, 4),
+            "kernel": "yk_mt_warmup_defer" if defer else "yk_mt_warmup<true, false>",
             "algorithmic_lane_ops_per_sample": round(alg_w / n, 2),
             "algorithmic_share_of_executed": round(alg_w / e_w, 4),
             "calls_consistent": round(executed(wb)[0] / e_w, 4),

@@ -155,6 +155,16 @@ static_assert(kClaimTail == 0 || (kClaimTail >= 64 && kClaimTail <= YK_CLAIM), "
 #ifndef YK_WG_HOLD
 #define YK_WG_HOLD 0
 #endif
+// the FP64 lens warm-up's retries drawn after its walks (yk_mt_warmup_defer) for launches of at
+// most YK_DEFER_SLOTS slots per warm-up wave (0: the rejection loop in line everywhere)
+#ifndef YK_LENS_DEFER
+#define YK_LENS_DEFER 1
+#endif
+#ifndef YK_DEFER_SLOTS
+#define YK_DEFER_SLOTS 4096
+#endif
+constexpr bool kLensDefer = YK_LENS_DEFER != 0;
+constexpr uint64_t kDeferSlots = YK_DEFER_SLOTS;
 constexpr uint32_t kFlagLinearScan = YK_FLAG_LINEAR_SCAN;
 constexpr uint32_t kFlagOneLane = YK_FLAG_ONE_LANE;
 constexpr uint32_t kFlagTrace = YK_FLAG_TRACE_RAYS;
@@ -452,15 +462,60 @@ struct WarmArgs {
   uint64_t n;  // sample slots in the launch
   void* out;
   uint32_t* counter;  // the launch's sample-slot counter: cleared here (the render waits for this kernel)
+  uint4* retry;         // yk_mt_warmup_defer: the lens retries, retry_cap records of 48 B per wave
+  uint32_t retry_cap, retry_pad;
 };
 
-template <bool kLens, bool kF32>
-__global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
+// Thin-lens retries after the walks (yk_mt_warmup_defer): a sample whose first random_in_unit_disk candidate is
+// rejected leaves its engine state (slot, seed, cursors, jitter canonicals) in its wave's ring and
+// the wave draws the further candidates for 64 such samples at a time once its grid-stride walks
+// are done, so no wave runs the rejection loop for its unluckiest lane (3.6 candidate draws per
+// wave-sample against 1.27 per sample).  A sample that finds its wave's ring full is handed to the
+// render as a start it makes itself (kNoStart), as a lens loop that runs out of lazy words is.
+// records per wave: the rejections of the wave's slots (p = 1 - pi/4) + 6 sigma + a batch
+inline uint32_t retry_cap_for(uint64_t slots_per_wave) {
+  const double m = 0.2146 * (double)slots_per_wave, sd = std::sqrt(m * 0.7854);
+  return ((uint32_t)(m + 6.0 * sd) + 64u + 63u) & ~63u;
+}
+__device__ __forceinline__ void retry_put(uint4* r, uint32_t i, const ykd::MtLane& g, double uc, double vc) {
+  r[0] = make_uint4(i, g.seed, g.a0, g.a1);
+  r[1] = make_uint4(g.b, g.j, 0u, 0u);
+  *(double2*)(r + 2) = make_double2(uc, vc);
+}
+// (agent-scope relaxed loads: global_load ... sc1, past this CU's L1 — another lane of the wave
+// wrote the record, and the ring's positions are rewritten)
+__device__ __forceinline__ uint64_t ld_l2(const uint4* r, int k) {
+  return __hip_atomic_load((const uint64_t*)r + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t retry_get(const uint4* r, ykd::MtLane& g, double& uc, double& vc) {
+  const uint64_t w0 = ld_l2(r, 0), w1 = ld_l2(r, 1), w2 = ld_l2(r, 2);
+  g.state = nullptr;
+  g.seed = (uint32_t)(w0 >> 32);
+  g.a0 = (uint32_t)w1;
+  g.a1 = (uint32_t)(w1 >> 32);
+  g.b = (uint32_t)w2;
+  g.j = (uint32_t)(w2 >> 32);
+  uc = __longlong_as_double((long long)ld_l2(r, 4));
+  vc = __longlong_as_double((long long)ld_l2(r, 5));
+  return (uint32_t)w0;
+}
+
+template <bool kLens, bool kF32, bool kDefer>
+__device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
+  constexpr uint32_t kWarmBlock = 256;  // (every warm-up launches 256-thread blocks)
   // (32-bit indices: a launch keeps its slots below 2^31 and the grid below 2^21 threads)
   const uint32_t n = (uint32_t)wa.n;
-  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t stride = gridDim.x * kWarmBlock;
   if (blockIdx.x == 0 && threadIdx.x == 0) *wa.counter = 0u;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  static_assert(!kDefer || (kLens && !kF32), "the deferred lens loop is the FP64 lens warm-up's");
+  // kDefer: this wave's ring and how many records it holds (every lane of the wave enqueues in
+  // step: a lane that has left the loop never holds the count alone, lane 0 leaves last)
+  uint4* const ring =
+      kDefer ? wa.retry + (size_t)__builtin_amdgcn_readfirstlane((blockIdx.x * kWarmBlock + threadIdx.x) >> 6) *
+                              wa.retry_cap * 3
+             : nullptr;
+  uint32_t rcount = 0;
+  for (uint32_t i = blockIdx.x * kWarmBlock + threadIdx.x; i < n; i += stride) {
     const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
     const uint32_t q = wa.order[pp];
     const uint32_t pix = q == kNoPixel ? 0u : q;
@@ -508,7 +563,30 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       const double uc = ykd::canonical<true>(g);  // source.cpp:162
       const double vc = ykd::canonical<true>(g);  // source.cpp:163
       double px = 0.0, py = 0.0;
-      if (kLens) {
+      if constexpr (kDefer) {
+        // the first candidate in line; a rejected sample goes to the ring while it has room
+        bool again = false;
+        if (!ykd::rng_lazy_ok(g, 4)) {
+          failed = true;
+        } else {
+          px = ykd::uniform<true>(g, -1, 1);
+          py = ykd::uniform<true>(g, -1, 1);
+          again = !(px * px + py * py < 1.0);
+        }
+        const unsigned long long m = __ballot(again);
+        const uint32_t nq = (uint32_t)__popcll(m);
+        const bool room = rcount + nq <= wa.retry_cap;
+        if (room) {
+          if (again) {
+            const uint32_t pos = rcount + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            retry_put(ring + 3 * pos, i, g, uc, vc);
+          }
+          rcount += nq;
+          if (again) continue;
+        } else if (again) {
+          failed = true;  // (the ring is full: the render kernel starts this sample itself)
+        }
+      } else if (kLens) {
         for (;;) {
           if (!ykd::rng_lazy_ok(g, 4)) {
             failed = true;
@@ -528,6 +606,68 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
       out[3] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
     }
   }
+  if constexpr (kDefer) {
+    // the ring: one more candidate for up to 64 records per trip, the rejected re-queued at its end
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t head = 0, cnt = __builtin_amdgcn_readfirstlane(rcount);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the records are in L2
+    while (cnt > 0u) {
+      const uint32_t take = min(cnt, 64u);
+      const bool act = lane < take;
+      ykd::MtLane g;
+      double uc = 0, vc = 0, px = 0, py = 0;
+      uint32_t i = 0;
+      bool again = false, failed = false;
+      if (act) {
+        uint32_t pos = head + lane;
+        pos = pos >= wa.retry_cap ? pos - wa.retry_cap : pos;
+        i = retry_get(ring + 3 * pos, g, uc, vc);
+        if (!ykd::rng_lazy_ok(g, 4)) {
+          failed = true;
+        } else {
+          px = ykd::uniform<true>(g, -1, 1);
+          py = ykd::uniform<true>(g, -1, 1);
+          again = !(px * px + py * py < 1.0);
+        }
+      }
+      head += take;
+      head = head >= wa.retry_cap ? head - wa.retry_cap : head;
+      cnt -= take;
+      const unsigned long long m = __ballot(again);
+      if (again) {
+        uint32_t pos = head + cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        pos = pos >= wa.retry_cap ? pos - wa.retry_cap : pos;
+        retry_put(ring + 3 * pos, i, g, uc, vc);
+      }
+      cnt += (uint32_t)__popcll(m);
+      if (act && !again) {
+        const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
+        const uint32_t q = wa.order[pp];
+        const uint32_t pix = q == kNoPixel ? 0u : q;
+        const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh);
+        const uint32_t xx = tile_col_x(wa.col_begin, wa.col_stride, wa.col_band, pix - tr * wa.Wt);
+        const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
+        uint4* const out = (uint4*)wa.out + 4 * (size_t)i;
+        out[3] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
+        v3 o, d;
+        camera_ray(wa.cam, wa.w_d, wa.inv_w, wa.h_d, wa.inv_h, wa.H, xx, y, uc, vc, kLens, px, py, o, d);
+        *(double2*)out = make_double2(o.x, o.y);
+        *(double2*)(out + 1) = make_double2(o.z, d.x);
+        *(double2*)(out + 2) = make_double2(d.y, d.z);
+      }
+      if (cnt > 0u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+}
+
+template <bool kLens, bool kF32>
+__global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
+  mt_warmup_body<kLens, kF32, false>(wa);
+}
+// the FP64 lens warm-up with its retries deferred, at 32 VGPRs: four of its waves beside the three
+// 128-VGPR render waves of a SIMD (the attribute counts gfx950's unified register file: twice)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16))) void yk_mt_warmup_defer(WarmArgs wa) {
+  mt_warmup_body<true, false, true>(wa);
 }
 
 // kSceneInLds: the BVH nodes, the leaf-ordered sphere geometry and the leaf→tuple ids are copied
@@ -1955,6 +2095,8 @@ struct ykgpu_context {
   DevTree t64, t32;  // the FP64 and FP32 kernels' trees over the current scene
   size_t scratch_lanes = 0;
   char* d_warm = nullptr;  // warm-up ring: a StartRec (FP64) or StartRecF (FP32) per sample slot
+  uint4* d_retry = nullptr;  // the FP64 warm-ups' lens-retry rings: retry_cap x 48 B per wave
+  size_t retry_cap = 0;
   double* d_col = nullptr;     // sample colours of one launch (kColStride doubles per slot)
   double* d_acc = nullptr;     // running per-pixel sums between launches
   size_t col_cap = 0, acc_cap = 0;
@@ -2448,6 +2590,24 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     break;
   }
   if (sched.size() > 1 && (rc = grow(ctx->d_acc, ctx->acc_cap, (size_t)nps * 3, sizeof(double)))) return rc;
+  // The FP64 lens warm-ups of launches with at most kDeferSlots slots per warm-up wave draw their
+  // lens retries after the walks (yk_mt_warmup_defer) from a ring per wave, sized to the largest
+  // such launch (the frame's 32-spp launches: 640 records, 1.0 GB); longer launches run the
+  // rejection loop in line (config 5's 121-spp launches: 7600 slots per wave, where the deferral
+  // measured 0.7% slower)
+  const bool lens_defer = kLensDefer && !x128 && !f32 && ctx->cam.lens_radius > 0;
+  auto wave_slots = [&](uint64_t nl) {
+    const uint64_t wb = std::min<uint64_t>((nl + 256 * kWarmSlots - 1) / (256 * kWarmSlots),
+                                           (uint64_t)ctx->cus * warm_per_cu(false));
+    return (nl + wb * 256 - 1) / (wb * 256) * 64;
+  };
+  uint32_t retry_cap = 0;  // records per wave
+  if (lens_defer)
+    for (const auto& l : sched)
+      if (wave_slots((uint64_t)nps * l.second) <= kDeferSlots)
+        retry_cap = std::max(retry_cap, retry_cap_for(wave_slots((uint64_t)nps * l.second)));
+  const size_t retry_n = (size_t)ctx->cus * warm_per_cu(false) * 4u * retry_cap * 3u;
+  if (retry_cap && (rc = grow(ctx->d_retry, ctx->retry_cap, retry_n, sizeof(uint4)))) return rc;
   KernelArgs ka;
   ka.cam = ctx->cam;
   ka.pad_a = 0;
@@ -2527,6 +2687,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   wa.row_stride = p->row_stride;
   wa.band_log2 = p->row_band_log2;
   wa.out = ctx->d_warm;
+  wa.retry = retry_cap ? ctx->d_retry : nullptr;
+  wa.retry_cap = retry_cap;
+  wa.retry_pad = 0;
   wa.lens = ctx->cam.lens_radius > 0 ? 1u : 0u;
   wa.H = p->image_height;
   wa.cam = ctx->cam;
@@ -2654,6 +2817,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
         hipLaunchKernelGGL((yk_mt_warmup<true, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else if (f32)
         hipLaunchKernelGGL((yk_mt_warmup<false, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
+      else if (wa.lens && wa.retry_cap && wave_slots(wa.n) <= kDeferSlots)
+        hipLaunchKernelGGL(yk_mt_warmup_defer, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else if (wa.lens)
         hipLaunchKernelGGL((yk_mt_warmup<true, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else
@@ -2746,6 +2911,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     cb += (uint64_t)kColRing * nps * K * kColStride * sizeof(double) + (x128 ? 0 : (uint64_t)kWarmRing * nps * K * welem);
     cb += (nlaunch > 1 ? (uint64_t)nps * 3 * sizeof(double) : 0) + (uint64_t)nps * sizeof(uint32_t);
     cb += nlaunch * sizeof(uint32_t) + kCounters * sizeof(unsigned long long);
+    if (retry_cap) cb += retry_n * sizeof(uint4);
     if (!x128) cb += 2 * lanes * ykd::kMtN * sizeof(uint32_t);
     cb += 2 * lanes * std::max(1u, p->max_depth > kStackRegs ? p->max_depth : 1u) * sizeof(uint16_t);
     const uint64_t npix = (uint64_t)p->row_count * tile_width(p);
@@ -2761,6 +2927,7 @@ uint64_t device_bytes(const ykgpu_context* ctx) {
   uint64_t b = ctx->t64.bytes + ctx->t32.bytes;
   if (ctx->d_geo) b += (uint64_t)ctx->nspheres * (sizeof(SphereGeo) + sizeof(SphereMat) + sizeof(float4));
   b += ctx->warm_cap + ctx->col_cap * sizeof(double) + ctx->acc_cap * sizeof(double);
+  b += ctx->retry_cap * sizeof(uint4);
   b += (uint64_t)ctx->order_slots * sizeof(uint32_t) + (uint64_t)ctx->counter_cap * sizeof(uint32_t);
   b += kCounters * sizeof(unsigned long long);
   if (ctx->d_mt) b += 2ull * ctx->scratch_lanes * ykd::kMtN * sizeof(uint32_t);
@@ -3001,6 +3168,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_clk);
   (void)hipFree(ctx->d_stats);
   (void)hipFree(ctx->d_warm);
+  (void)hipFree(ctx->d_retry);
   (void)hipFree(ctx->d_order);
   (void)hipFree(ctx->d_col);
   (void)hipFree(ctx->d_acc);
