@@ -2606,8 +2606,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     for (const auto& l : sched)
       if (wave_slots((uint64_t)nps * l.second) <= kDeferSlots)
         retry_cap = std::max(retry_cap, retry_cap_for(wave_slots((uint64_t)nps * l.second)));
-  const size_t retry_n = (size_t)ctx->cus * warm_per_cu(false) * 4u * retry_cap * 3u;
-  if (retry_cap && (rc = grow(ctx->d_retry, ctx->retry_cap, retry_n, sizeof(uint4)))) return rc;
+  size_t retry_n = (size_t)ctx->cus * warm_per_cu(false) * 4u * retry_cap * 3u;
+  if (retry_cap && (rc = grow(ctx->d_retry, ctx->retry_cap, retry_n, sizeof(uint4)))) {
+    if (rc != YK_ERR_NOMEM) return rc;
+    // a device short of memory runs the rejection loop in line instead (slower, never fatal)
+    (void)hipGetLastError();
+    retry_cap = 0;
+    retry_n = 0;
+  }
   KernelArgs ka;
   ka.cam = ctx->cam;
   ka.pad_a = 0;
