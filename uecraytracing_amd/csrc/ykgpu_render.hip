@@ -666,7 +666,10 @@ __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
 }
 // the FP64 lens warm-up with its retries deferred, at 32 VGPRs: four of its waves beside the three
 // 128-VGPR render waves of a SIMD (the attribute counts gfx950's unified register file: twice)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(16))) void yk_mt_warmup_defer(WarmArgs wa) {
+#ifndef YK_DEFER_VGPRS
+#define YK_DEFER_VGPRS 32
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(YK_DEFER_VGPRS / 2))) void yk_mt_warmup_defer(WarmArgs wa) {
   mt_warmup_body<true, false, true>(wa);
 }
 
