@@ -500,7 +500,9 @@ __device__ __forceinline__ uint32_t retry_get(const uint4* r, ykd::MtLane& g, do
   return (uint32_t)w0;
 }
 
-template <bool kLens, bool kF32, bool kDefer>
+// kIlp: the seed walks of kIlp slots interleaved per lane (i, i + stride, ...; the walk is a
+// chain of dependent instructions), their starts then one after the other
+template <bool kLens, bool kF32, bool kDefer, uint32_t kIlp>
 __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
   constexpr uint32_t kWarmBlock = 256;  // (every warm-up launches 256-thread blocks)
   // (32-bit indices: a launch keeps its slots below 2^31 and the grid below 2^21 threads)
@@ -515,28 +517,21 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
                               wa.retry_cap * 3
              : nullptr;
   uint32_t rcount = 0;
-  for (uint32_t i = blockIdx.x * kWarmBlock + threadIdx.x; i < n; i += stride) {
+  // slot i's pixel (xx, y) and seed
+  auto slot_seed = [&](uint32_t i, uint32_t& xx, uint32_t& y) -> uint32_t {
     const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
     const uint32_t q = wa.order[pp];
     const uint32_t pix = q == kNoPixel ? 0u : q;
     const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh);
-    const uint32_t xx = tile_col_x(wa.col_begin, wa.col_stride, wa.col_band, pix - tr * wa.Wt);
-    const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
-    const uint32_t seed = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
-    uint32_t x[1] = {seed};
-    ykd::mt_walk397xn<1>(x);
-#ifdef YK_WALK_SENS
-    // (sensitivity probe, never in the product: YK_WALK_SENS more walks of a perturbed seed, their
-    // result folded in as a no-op the compiler cannot prove)
-    for (int r_ = 0; r_ < YK_WALK_SENS; ++r_) {
-      uint32_t z[1] = {seed ^ (0x9e3779b9u + (uint32_t)r_)};
-      ykd::mt_walk397xn<1>(z);
-      x[0] ^= (z[0] == 0x12345678u && seed == 0x9abcdef0u) ? 1u : 0u;
-    }
-#endif
+    xx = tile_col_x(wa.col_begin, wa.col_stride, wa.col_band, pix - tr * wa.Wt);
+    y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
+    return ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
+  };
+  // the start of slot i after its walk: draws, lens, camera ray, record
+  auto start_slot = [&](uint32_t i, uint32_t xx, uint32_t y, uint32_t seed, uint32_t x397) {
     ykd::MtLane g;
     g.state = nullptr;
-    ykd::mt_start_from(g, seed, x[0]);
+    ykd::mt_start_from(g, seed, x397);
     bool failed = false;  // the lens loop would reach the scratch engine's words
     if constexpr (kF32) {
       const float uc = ykf::canonical<true>(g);  // source.cpp:162 with T = float
@@ -582,7 +577,7 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
             retry_put(ring + 3 * pos, i, g, uc, vc);
           }
           rcount += nq;
-          if (again) continue;
+          if (again) return;
         } else if (again) {
           failed = true;  // (the ring is full: the render kernel starts this sample itself)
         }
@@ -604,6 +599,45 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
       *(double2*)(out + 1) = make_double2(o.z, d.x);
       *(double2*)(out + 2) = make_double2(d.y, d.z);
       out[3] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
+    }
+  };
+  if constexpr (kIlp > 1) {
+    for (uint32_t i = blockIdx.x * kWarmBlock + threadIdx.x; i < n; i += kIlp * stride) {
+      uint32_t xx, y, x[kIlp];
+#pragma unroll
+      for (uint32_t k = kIlp - 1; k > 0; --k) {
+        const uint32_t ik = i + k * stride;
+        x[k] = slot_seed(ik < n ? ik : i, xx, y);
+      }
+      const uint32_t seed = slot_seed(i, xx, y);
+      x[0] = seed;
+      ykd::mt_walk397xn<kIlp>(x);
+      start_slot(i, xx, y, seed, x[0]);
+#pragma unroll
+      for (uint32_t k = 1; k < kIlp; ++k) {
+        const uint32_t ik = i + k * stride;
+        if (ik < n) {
+          const uint32_t sk = slot_seed(ik, xx, y);
+          start_slot(ik, xx, y, sk, x[k]);
+        }
+      }
+    }
+  } else {
+    for (uint32_t i = blockIdx.x * kWarmBlock + threadIdx.x; i < n; i += stride) {
+      uint32_t xx, y;
+      const uint32_t seed = slot_seed(i, xx, y);
+      uint32_t x[1] = {seed};
+      ykd::mt_walk397xn<1>(x);
+#ifdef YK_WALK_SENS
+      // (sensitivity probe, never in the product: YK_WALK_SENS more walks of a perturbed seed, their
+      // result folded in as a no-op the compiler cannot prove)
+      for (int r_ = 0; r_ < YK_WALK_SENS; ++r_) {
+        uint32_t z[1] = {seed ^ (0x9e3779b9u + (uint32_t)r_)};
+        ykd::mt_walk397xn<1>(z);
+        x[0] ^= (z[0] == 0x12345678u && seed == 0x9abcdef0u) ? 1u : 0u;
+      }
+#endif
+      start_slot(i, xx, y, seed, x[0]);
     }
   }
   if constexpr (kDefer) {
@@ -660,17 +694,27 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
   }
 }
 
+// Walks per lane: the deferred FP64 lens warm-up (the headline frame's) walks four slots at once at
+// 48 VGPRs, so two of its waves share a SIMD with the three render waves (eight walk chains per
+// SIMD instead of four: bench -0.9%, r05_ab/walk/); the other warm-ups walk one
+#ifndef YK_WALK_ILP
+#define YK_WALK_ILP 4
+#endif
+#ifndef YK_WALK_ILP_INLINE
+#define YK_WALK_ILP_INLINE 1
+#endif
+constexpr uint32_t kWalkIlp = YK_WALK_ILP, kWalkIlpInline = YK_WALK_ILP_INLINE;
 template <bool kLens, bool kF32>
 __global__ __launch_bounds__(256) void yk_mt_warmup(WarmArgs wa) {
-  mt_warmup_body<kLens, kF32, false>(wa);
+  mt_warmup_body<kLens, kF32, false, kWalkIlpInline>(wa);
 }
-// the FP64 lens warm-up with its retries deferred, at 32 VGPRs: four of its waves beside the three
+// the FP64 lens warm-up with its retries deferred, at 48 VGPRs: two of its waves beside the three
 // 128-VGPR render waves of a SIMD (the attribute counts gfx950's unified register file: twice)
 #ifndef YK_DEFER_VGPRS
-#define YK_DEFER_VGPRS 32
+#define YK_DEFER_VGPRS 48
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(YK_DEFER_VGPRS / 2))) void yk_mt_warmup_defer(WarmArgs wa) {
-  mt_warmup_body<true, false, true>(wa);
+  mt_warmup_body<true, false, true, kWalkIlp>(wa);
 }
 
 // kSceneInLds: the BVH nodes, the leaf-ordered sphere geometry and the leaf→tuple ids are copied
@@ -2437,6 +2481,20 @@ uint32_t warm_per_cu(bool f32) {
   if (const char* e = ab_knob("YKGPU_WARM_PER_CU")) per_cu = (uint32_t)std::max(1, std::atoi(e));
   return per_cu;
 }
+// A warm-up's blocks for n slots, at most cap: each thread walks n / grid slots, at least
+// kWarmSlots; with ilp walks per lane the grid is trimmed so that a thread's slot count is a
+// multiple of ilp (no lane walks a chain for a slot it does not have, but in the last blocks)
+#ifndef YK_WARM_TRIM
+#define YK_WARM_TRIM 1
+#endif
+inline uint32_t warm_blocks_for(uint64_t n, uint64_t cap, uint32_t ilp) {
+  uint64_t wb = std::min<uint64_t>((n + 256 * kWarmSlots - 1) / (256 * kWarmSlots), cap);
+  if (YK_WARM_TRIM && ilp > 1 && wb > 0) {
+    const uint64_t per = 256ull * ilp, it = (n + wb * per - 1) / (wb * per);
+    wb = (n + per * it - 1) / (per * it);
+  }
+  return (uint32_t)wb;
+}
 
 int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, double* sums_dev,
            hipStream_t st) {
@@ -2600,8 +2658,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // measured 0.7% slower)
   const bool lens_defer = kLensDefer && !x128 && !f32 && ctx->cam.lens_radius > 0;
   auto wave_slots = [&](uint64_t nl) {
-    const uint64_t wb = std::min<uint64_t>((nl + 256 * kWarmSlots - 1) / (256 * kWarmSlots),
-                                           (uint64_t)ctx->cus * warm_per_cu(false));
+    const uint64_t wb = warm_blocks_for(nl, (uint64_t)ctx->cus * warm_per_cu(false), kWalkIlp);
     return (nl + wb * 256 - 1) / (wb * 256) * 64;
   };
   uint32_t retry_cap = 0;  // records per wave
@@ -2818,15 +2875,15 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)((g0 + c) % kWarmRing) * nps * K * welem;
     wa.counter = ctx->d_counter + (g0 + c) % kWarmRing;
-    const uint32_t wblocks =
-        (uint32_t)std::min<uint64_t>((wa.n + 256 * kWarmSlots - 1) / (256 * kWarmSlots), (uint64_t)ctx->cus * warm_per_cu(f32));
+    const bool defer = !x128 && !f32 && wa.lens && wa.retry_cap && wave_slots(wa.n) <= kDeferSlots;
+    const uint32_t wblocks = warm_blocks_for(wa.n, (uint64_t)ctx->cus * warm_per_cu(f32), defer ? kWalkIlp : kWalkIlpInline);
     YK_HIP(hipEventRecord(ev[0], ctx->aux));
     if (!x128) {
       if (f32 && wa.lens)
         hipLaunchKernelGGL((yk_mt_warmup<true, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else if (f32)
         hipLaunchKernelGGL((yk_mt_warmup<false, true>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
-      else if (wa.lens && wa.retry_cap && wave_slots(wa.n) <= kDeferSlots)
+      else if (defer)
         hipLaunchKernelGGL(yk_mt_warmup_defer, dim3(wblocks), dim3(256), 0, ctx->aux, wa);
       else if (wa.lens)
         hipLaunchKernelGGL((yk_mt_warmup<true, false>), dim3(wblocks), dim3(256), 0, ctx->aux, wa);
