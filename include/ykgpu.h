@@ -204,7 +204,7 @@ typedef struct yk_render_stats {
                               back when it needs less than half                            */
   uint64_t call_bytes;     /* device memory THIS call needed (the same items sized to it):
                               1920x1080x512 FP64 ~19.1 GB; the 8-GPU split's tile of 3840x2160x1024
-                              (480 columns) ~10.4 GB; 1920x1080x4096 (config 5) ~71 GB      */
+                              (480 columns) ~10.5 GB; 1920x1080x4096 (config 5) ~71 GB      */
   double sclk_mhz;         /* the shader clock the render launches ran at: s_memtime over
                               s_memrealtime (100 MHz) of one wave per launch, averaged      */
   uint32_t launch_spp;     /* samples per pixel of the call's largest launch (ABI 11)        */

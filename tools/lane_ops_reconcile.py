@@ -23,13 +23,15 @@ the same samples.  Per kernel:
     VALU), the walk loop (12 VALU per 4 steps, 99 trips), the rest of the start's draws and the
     camera ray (146), and 108 per thin-lens rejection iteration (4 words each: the iterations are
     (start words - 4) / 4 per sample, from the work counters);
-  - yk_mt_warmup_defer (the retries drawn after the walks, DEFER_*; round 5's production warm-up
+  - yk_mt_warmup_defer (the retries drawn after the walks, DEFER["k1"]; round 5's production warm-up
     for launches of <= 4096 slots per wave): per sample the loop body through the first
     candidate (1424: index math, seed, walk, the start's draws, the candidate, the latch), then
     the camera ray and StartRec (48) for a sample accepted there or the ring store (10) for one
     rejected; per retry the ring read and the candidate (7 + 9 + 106), then the ring store (9) or
     the camera ray (71).  Rejections at the first candidate are taken at their expectation
     (1 - pi/4 per sample); every retry ends a rejection, so retries = candidates - samples.
+    Since r05af the kernel walks four slots per lane (DEFER["k4"], the default; YK_DEFER_MODEL=k1
+    re-reads the r05v passes with the one-walk build's counts).
 * The algorithmic lane-ops (uecraytracing_amd/flops.py lane_ops) over the executed ones: how much
   of what the VALU executes is the reference's own arithmetic.
 """
@@ -50,11 +52,21 @@ WARM_FIXED = 26 + 5 + 31 + 115
 WARM_WALK_LOOP = 12 * 99
 WARM_LENS_ITER = 108
 
-# yk_mt_warmup_defer (ISA of the round-5 build: VALU per basic block, see the docstring)
-DEFER_MAIN = 23 + 3 + 5 + 12 * 99 + 200 + 3 + 2
-DEFER_FINISH_MAIN, DEFER_PUT_MAIN = 48, 10
-DEFER_RETRY = 7 + 9 + 106
-DEFER_PUT_RETRY, DEFER_FINISH_RETRY = 9, 71
+# yk_mt_warmup_defer (VALU per basic block, see the docstring), per build:
+#  "k1" (r05v: one walk per lane):
+#  "k4" (since r05af: four walks per lane): per 4-slot trip the four slots' index math and seed
+#       (117), the walks' first step (14) and loop (48 per 4 steps, 99 trips), the first slot's
+#       start through its candidate (203), for each of the other three its index math and seed
+#       again (26) and its start (206), the latch (4); per sample accepted at once the camera ray
+#       and StartRec (52 + 2), per rejection the ring store (10 + 1); the drain as k1 but the
+#       camera ray (74)
+DEFER = {
+    "k1": dict(main=23 + 3 + 5 + 12 * 99 + 200 + 3 + 2, finish_main=48, put_main=10, retry=7 + 9 + 106,
+               put_retry=9, finish_retry=71),
+    "k4": dict(main=(117 + 14 + 48 * 99 + 203 + 3 * (26 + 206) + 4) / 4.0, finish_main=54, put_main=11,
+               retry=122, put_retry=9, finish_retry=74),
+}
+DEFER_BUILD = os.environ.get("YK_DEFER_MODEL", "k4")
 P_REJECT = 1.0 - 3.141592653589793 / 4.0
 
 RENDER = "yk_render_persistent<true, "
@@ -128,8 +140,9 @@ def main():
     if defer:
         rej1 = P_REJECT * n
         retries = max(0.0, lens_iters - n)
-        warm_model = (n * DEFER_MAIN + (n - rej1) * DEFER_FINISH_MAIN + rej1 * DEFER_PUT_MAIN
-                      + retries * DEFER_RETRY + (retries - rej1) * DEFER_PUT_RETRY + rej1 * DEFER_FINISH_RETRY)
+        m = DEFER[DEFER_BUILD]
+        warm_model = (n * m["main"] + (n - rej1) * m["finish_main"] + rej1 * m["put_main"]
+                      + retries * m["retry"] + (retries - rej1) * m["put_retry"] + rej1 * m["finish_retry"])
     else:
         warm_model = n * (WARM_FIXED + WARM_WALK_LOOP) + lens_iters * WARM_LENS_ITER
     e_w, lu_w = executed(wa)
