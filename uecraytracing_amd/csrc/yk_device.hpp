@@ -270,11 +270,22 @@ __device__ __forceinline__ void mt_walk397xn(uint32_t (&x)[N]) {
 }
 
 // The rare path: the real engine in global scratch (seed :69-81, M_gen_rand :114-131).
-// Out of line and by value so the hot path keeps the lane's cursors in registers.
-__device__ __noinline__ uint32_t mt_slow(uint32_t* st, uint32_t seed, uint32_t j) {
+// Out of line and by value so the hot path keeps the lane's cursors in registers.  At its first
+// call (j = 227) cursor A holds x_227, and the seed x_0 is recovered from it: a seeding step
+// x_i = C (u ^ u >> 30) + i is invertible (C odd: t = (x_i - i) C^-1 = u ^ u >> 30, and u = t ^
+// t >> 30, since the xor changes only bits 0-1), so the lane never carries its seed.
+constexpr uint32_t kMtSeedMulInv = 0x9638806du;  // 1812433253^-1 mod 2^32
+__device__ __forceinline__ uint32_t mt_seed_from(uint32_t x, uint32_t i) {  // x_i -> x_0
+  for (; i > 0; --i) {
+    const uint32_t t = (x - i) * kMtSeedMulInv;
+    x = t ^ (t >> 30);
+  }
+  return x;
+}
+__device__ __noinline__ uint32_t mt_slow(uint32_t* st, uint32_t x227, uint32_t j) {
   const uint32_t idx = j % kMtN;
   if (j == kLazyDraws) {
-    uint32_t x = seed;
+    uint32_t x = mt_seed_from(x227, kLazyDraws);
     st[0] = x;
     for (uint32_t i = 1; i < kMtN; ++i) {
       x = mt_seed_step(x, i);
@@ -310,7 +321,7 @@ __device__ __forceinline__ uint32_t mt_next(MtLane& g) {
     g.a1 = mt_seed_step(g.a1, g.j + 2);
     g.b = mt_seed_step(g.b, g.j + kMtM + 1);
   } else {
-    z = mt_slow(g.state, g.seed, g.j);
+    z = mt_slow(g.state, g.a0, g.j);  // (a0 = x_227 at the first call)
   }
   ++g.j;
   return mt_temper(z);

@@ -437,6 +437,10 @@ struct alignas(16) StartRecF {
 };
 static_assert(sizeof(StartRecF) == 48, "StartRecF layout");
 constexpr uint32_t kNoStart = 0xffffffffu;
+// j == kPadSlot: the slot is an empty slot of an edge block (kNoPixel in the processing order), so
+// the render tells it from its StartRec alone and reads the order only for a start it makes itself
+constexpr uint32_t kPadSlot = 0xfffffffeu;
+constexpr uint32_t kPadX = 0xffffffffu;  // (the warm-up's column of such a slot)
 
 // Seed walk and start of every sample of a launch, fully coherent, one sample per thread
 // (grid-stride): the 397-step walk, then the start's draws with the lazy cursors (yk_device.hpp)
@@ -517,7 +521,7 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
                               wa.retry_cap * 3
              : nullptr;
   uint32_t rcount = 0;
-  // slot i's pixel (xx, y) and seed
+  // slot i's pixel (xx, y) and seed; an empty slot gets column kPadX (its record is marked)
   auto slot_seed = [&](uint32_t i, uint32_t& xx, uint32_t& y) -> uint32_t {
     const uint32_t sl = fdiv(i, wa.nps_m, wa.nps_sh), pp = i - sl * wa.npix_slots;
     const uint32_t q = wa.order[pp];
@@ -525,7 +529,9 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
     const uint32_t tr = fdiv(pix, wa.w_m, wa.w_sh);
     xx = tile_col_x(wa.col_begin, wa.col_stride, wa.col_band, pix - tr * wa.Wt);
     y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
-    return ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
+    const uint32_t seed = ykd::sample_seed(wa.seed_mode, wa.seed_key, wa.seed0, y, xx, wa.W, wa.spp, wa.s0 + sl);
+    xx = q == kNoPixel ? kPadX : xx;
+    return seed;
   };
   // the start of slot i after its walk: draws, lens, camera ray, record
   auto start_slot = [&](uint32_t i, uint32_t xx, uint32_t y, uint32_t seed, uint32_t x397) {
@@ -553,7 +559,7 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
       uint4* const out = (uint4*)wa.out + 3 * (size_t)i;
       *(float4*)out = make_float4(o.x, o.y, o.z, d.x);
       *(float4*)(out + 1) = make_float4(d.y, d.z, 0.0f, 0.0f);
-      out[2] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
+      out[2] = make_uint4(g.a0, g.a1, g.b, xx == kPadX ? kPadSlot : failed ? kNoStart : g.j);
     } else {
       const double uc = ykd::canonical<true>(g);  // source.cpp:162
       const double vc = ykd::canonical<true>(g);  // source.cpp:163
@@ -598,7 +604,7 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
       *(double2*)out = make_double2(o.x, o.y);
       *(double2*)(out + 1) = make_double2(o.z, d.x);
       *(double2*)(out + 2) = make_double2(d.y, d.z);
-      out[3] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
+      out[3] = make_uint4(g.a0, g.a1, g.b, xx == kPadX ? kPadSlot : failed ? kNoStart : g.j);
     }
   };
   if constexpr (kIlp > 1) {
@@ -682,7 +688,7 @@ __device__ __forceinline__ void mt_warmup_body(const WarmArgs& wa) {
         const uint32_t xx = tile_col_x(wa.col_begin, wa.col_stride, wa.col_band, pix - tr * wa.Wt);
         const uint32_t y = tile_row_y(wa.row_begin, wa.row_stride, wa.band_log2, tr);
         uint4* const out = (uint4*)wa.out + 4 * (size_t)i;
-        out[3] = make_uint4(g.a0, g.a1, g.b, failed ? kNoStart : g.j);
+        out[3] = make_uint4(g.a0, g.a1, g.b, q == kNoPixel ? kPadSlot : failed ? kNoStart : g.j);
         v3 o, d;
         camera_ray(wa.cam, wa.w_d, wa.inv_w, wa.h_d, wa.inv_h, wa.H, xx, y, uc, vc, kLens, px, py, o, d);
         *(double2*)out = make_double2(o.x, o.y);
@@ -963,15 +969,14 @@ void yk_render_persistent(KernelArgs ka) {
 
     // ---- start sample s of the pixel: seed, jitter, camera ray (source.cpp:154-165) ------
     bool start = !in_path;
-    uint32_t qpix = 0;
-    // the slot's pixel and (mt19937) its StartRec issued together and waited for once: tested
-    // one after the other they cost three dependent memory round trips per sample start (the
-    // record's j, then its other words under the test).  Every slot of the launch, padded ones
-    // included, has a record, so the read is in bounds.
+    // mt19937: the slot's StartRec, its four loads issued together and waited for once (every
+    // slot of the launch, empty ones included, has a record, so the read is in bounds); it says
+    // whether the slot is empty (kPadSlot) and holds the whole start, so neither the processing
+    // order nor the pixel's seed is read here — the scratch engine recovers the seed from its
+    // cursor (mt_slow).  xor128: the slot's pixel
     uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0}, rq3 = {0, 0, 0, 0};
+    uint32_t qpix = 0;
     if (start) {
-      const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
-      qpix = ka.order[slot - sl * ka.npix_slots];
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
         const uint4* rp = (const uint4*)ka.start + 4u * slot;
         rq0 = rp[0];
@@ -980,24 +985,22 @@ void yk_render_persistent(KernelArgs ka) {
         rq3 = rp[3];
         asm volatile("" ::"v"(rq0.x), "v"(rq0.y), "v"(rq0.z), "v"(rq0.w), "v"(rq1.x), "v"(rq1.y),
                      "v"(rq1.z), "v"(rq1.w), "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(rq3.x),
-                     "v"(rq3.y), "v"(rq3.z), "v"(rq3.w), "v"(qpix));
+                     "v"(rq3.y), "v"(rq3.z), "v"(rq3.w));
+        start = rq3.w != kPadSlot;  // an empty slot of an edge block: take another next trip
+      } else {
+        const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
+        qpix = ka.order[slot - sl * ka.npix_slots];
+        start = qpix != kNoPixel;
       }
-      start = qpix != kNoPixel;  // an empty slot of an edge block: take another next trip
     }
     if (start) {
       // The start — the jitter canonicals, the lens point and the camera ray — and the engine
       // after its draws: precomputed for mt19937 by yk_mt_warmup (StartRec), so the divergent
       // loop only loads them; xor128, and the (never seen) record the warm-up could not
       // complete, start here
-      const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
-      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh);
-      const uint32_t x = tile_col_x(ka.col_begin, ka.col_stride, ka.col_band, qpix - tr * ka.Wt);
-      const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
-      // seed (uint32 wrap, source.cpp:154-158)
-      const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
       bool pre = false;
       if constexpr (std::is_same<Gen, ykd::MtLane>::value) {
-        StartRec r;  // (loaded above with the pixel)
+        StartRec r;  // (loaded above)
         __builtin_memcpy((char*)&r, &rq0, 16);
         __builtin_memcpy((char*)&r + 16, &rq1, 16);
         __builtin_memcpy((char*)&r + 32, &rq2, 16);
@@ -1005,7 +1008,6 @@ void yk_render_persistent(KernelArgs ka) {
         pre = r.j != kNoStart;
         if (pre) {
           if (kCount) n_swords += r.j;
-          g.seed = seed;  // (the scratch engine's seeding needs it)
           g.a0 = r.a0;
           g.a1 = r.a1;
           g.b = r.b;
@@ -1015,6 +1017,14 @@ void yk_render_persistent(KernelArgs ka) {
         }
       }
       if (!pre) {
+        // the pixel and its seed (uint32 wrap, source.cpp:154-158)
+        const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
+        if constexpr (std::is_same<Gen, ykd::MtLane>::value) qpix = ka.order[slot - sl * ka.npix_slots];
+        const uint32_t s = ka.s0 + sl;
+        const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh);
+        const uint32_t x = tile_col_x(ka.col_begin, ka.col_stride, ka.col_band, qpix - tr * ka.Wt);
+        const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
+        const uint32_t seed = ykd::sample_seed(kRandomSeed ? 1u : 0u, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
         const bool lens = ka.cam.lens_radius > 0;
         rng_start_full(g, seed);
         const double uc = ykd::canonical<true>(g);  // (a fresh engine: its first words never need the scratch engine)
