@@ -1639,28 +1639,25 @@ void yk_render_f32(KernelArgs ka) {
     bool start = !in_path;
     uint32_t qpix = 0;
     // mt19937: the start (draws and camera<float> ray) comes precomputed (yk_mt_warmup<lens,
-    // true>: StartRecF), loaded with the pixel as in the FP64 kernel
+    // true>: StartRecF), which alone says whether the slot is empty, as in the FP64 kernel
     constexpr bool kRec = std::is_same<Gen, ykd::MtLane>::value;
     uint4 rq0 = {0, 0, 0, 0}, rq1 = {0, 0, 0, 0}, rq2 = {0, 0, 0, 0};
     if (start) {
-      const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
-      qpix = ka.order[slot - sl * ka.npix_slots];
       if constexpr (kRec) {
         const uint4* rp = (const uint4*)ka.start + 3u * slot;
         rq0 = rp[0];
         rq1 = rp[1];
         rq2 = rp[2];
         asm volatile("" ::"v"(rq0.x), "v"(rq0.y), "v"(rq0.z), "v"(rq0.w), "v"(rq1.x), "v"(rq1.y),
-                     "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w), "v"(qpix));
+                     "v"(rq2.x), "v"(rq2.y), "v"(rq2.z), "v"(rq2.w));
+        start = rq2.w != kPadSlot;
+      } else {
+        const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
+        qpix = ka.order[slot - sl * ka.npix_slots];
+        start = qpix != kNoPixel;
       }
-      start = qpix != kNoPixel;
     }
     if (start) {
-      const uint32_t s = ka.s0 + fdiv(slot, ka.nps_m, ka.nps_sh);
-      const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh);
-      const uint32_t x = tile_col_x(ka.col_begin, ka.col_stride, ka.col_band, qpix - tr * ka.Wt);
-      const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
-      const uint32_t seed = ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
       bool pre = false;
       if constexpr (kRec) {
         StartRecF r;
@@ -1670,7 +1667,6 @@ void yk_render_f32(KernelArgs ka) {
         pre = r.j != kNoStart;
         if (pre) {
           if (kCount) n_swords += r.j;
-          g.seed = seed;
           g.a0 = r.a0;
           g.a1 = r.a1;
           g.b = r.b;
@@ -1680,6 +1676,13 @@ void yk_render_f32(KernelArgs ka) {
         }
       }
       if (!pre) {
+        const uint32_t sl = fdiv(slot, ka.nps_m, ka.nps_sh);
+        if constexpr (kRec) qpix = ka.order[slot - sl * ka.npix_slots];
+        const uint32_t s = ka.s0 + sl;
+        const uint32_t tr = fdiv(qpix, ka.w_m, ka.w_sh);
+        const uint32_t x = tile_col_x(ka.col_begin, ka.col_stride, ka.col_band, qpix - tr * ka.Wt);
+        const uint32_t y = tile_row_y(ka.row_begin, ka.row_stride, ka.band_log2, tr);
+        const uint32_t seed = ykd::sample_seed(ka.seed_mode, ka.seed_key, ka.seed0, y, x, ka.W, ka.spp, s);
         const bool lens = ka.cam.lens_radius > 0;  // (decided in double, as for the warm-up)
         rng_start_full(g, seed);
         const float uc = f_uniform01(g);
