@@ -727,34 +727,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(YK_DEFER_VGPRS 
 // into LDS by each workgroup once (33 KB for the 485-sphere scene), so a node visit is four
 // ds_read_b128 instead of four dependent L2 round trips.  Larger scenes read them from global.
 
-// A sample's colour record: r, g, b and the ids of the unwind's last four attenuations as one
-// aligned 32-byte record per sample slot (two 16-byte stores, the whole record in one 32-byte
-// sector), in a colour buffer of the launch.
+// A sample's colour record: r, g, b as one aligned 32-byte record per sample slot (one 16-byte
+// and one 8-byte store, the whole record in one 32-byte sector), in a colour buffer of the launch.
 // yk_reduce_samples reads the records of consecutive slots, coalesced.  (Round 4 tried writing
 // the colour over the slot's own StartRec instead — no colour buffer at all — and the frame got
 // 3% slower: 174.1 -> 179.5 ms, profiles/r04_ab/; the reduce then reads 24 of every 64 bytes.)
 constexpr size_t kColStride = 4;
-#ifndef YK_UNWIND_DEFER
-#define YK_UNWIND_DEFER 1
-#endif
-// kUnwindDefer: the outermost (up to) four scatterings of a path are unwound by the reduce, not by
-// the render's divergent loop: the record's fourth word holds their material ids, 16 bits each,
-// the next to multiply in the low bits, 0xffff for none
-constexpr bool kUnwindDefer = YK_UNWIND_DEFER != 0;
-constexpr uint32_t kUnwindInReduce = 4;
 __device__ __forceinline__ void colour_store(double* col, uint32_t slot, double r, double g, double b) {
   double* rec = col + (size_t)slot * kColStride;
   *(double2*)rec = make_double2(r, g);
-  if constexpr (kUnwindDefer)
-    *(double2*)(rec + 2) = make_double2(b, __longlong_as_double(-1ll));
-  else
-    rec[2] = b;
-}
-__device__ __forceinline__ void colour_store_ids(double* col, uint32_t slot, double r, double g, double b,
-                                                 uint64_t ids) {
-  double* rec = col + (size_t)slot * kColStride;
-  *(double2*)rec = make_double2(r, g);
-  *(double2*)(rec + 2) = make_double2(b, __longlong_as_double((long long)ids));
+  rec[2] = b;
 }
 
 // Ordered sum of a launch's sample colours per pixel: pixel_color of source.cpp:137-167 is the
@@ -763,7 +745,6 @@ __device__ __forceinline__ void colour_store_ids(double* col, uint32_t slot, dou
 // truncate.  One thread per processing slot, coalesced over the SoA colours.
 struct ReduceArgs {
   const double* col;  // col[(s_local * npix_slots + p) * kColStride + c]
-  const SphereMat* mat;  // (kUnwindDefer) the attenuations the reduce multiplies in
   double* acc;        // running sums, acc[c * npix_slots + p]
   const uint32_t* order;
   uint8_t* rgb;
@@ -779,28 +760,8 @@ __device__ __forceinline__ void reduce_slot(const ReduceArgs& ra, uint32_t p) {
   for (int c = 0; c < 3; ++c) a[c] = ra.first ? 0.0 : ra.acc[(size_t)c * ra.npix_slots + p];
   for (uint32_t k = 0; k < ra.ks; ++k) {
     const size_t i = (size_t)k * ra.npix_slots + p;
-    if constexpr (kUnwindDefer) {
-      // the rest of the path's unwind (raytracer.hpp:31), innermost first, as the render's loop
-      const double2 rg = *(const double2*)(ra.col + i * kColStride);
-      const double2 bw = *(const double2*)(ra.col + i * kColStride + 2);
-      double L[3] = {rg.x, rg.y, bw.x};
-      const uint64_t ids = (uint64_t)__double_as_longlong(bw.y);
 #pragma unroll
-      for (uint32_t j = 0; j < kUnwindInReduce; ++j) {
-        const uint32_t id = (uint32_t)(ids >> (16 * j)) & 0xffffu;
-        if (id != 0xffffu) {
-          const SphereMat m = ra.mat[id];
-          L[0] = m.ar * L[0];
-          L[1] = m.ag * L[1];
-          L[2] = m.ab * L[2];
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 3; ++c) a[c] = a[c] + L[c];
-    } else {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[i * kColStride + c];
-    }
+    for (int c = 0; c < 3; ++c) a[c] = a[c] + ra.col[i * kColStride + c];
   }
   if (!ra.last) {
 #pragma unroll
@@ -1468,7 +1429,7 @@ void yk_render_persistent(KernelArgs ka) {
         --nstk;
         return id;
       };
-      while (nstk > (kUnwindDefer ? kUnwindInReduce : 0u)) {
+      while (nstk > 0) {
         const SphereMat m = mat[pop()];
         L_r = m.ar * L_r;
         L_g = m.ag * L_g;
@@ -1477,15 +1438,7 @@ void yk_render_persistent(KernelArgs ka) {
       if (ykd::mt_used_fallback(g)) ++n_fb;
       if (kCount) n_words += ykd::rng_words(g), n_twist += ykd::rng_twists(g);
       // the sample's colour; yk_reduce_samples adds them in sample order
-      if constexpr (kUnwindDefer) {
-        // the outermost nstk <= 4 attenuation ids, next to pop in the low bits, left to the reduce
-        uint64_t ids = ((uint64_t)st1 << 32) | st0;
-        if (nstk < kUnwindInReduce) ids |= ~0ull << (16 * nstk);
-        colour_store_ids(ka.col, slot, L_r, L_g, L_b, ids);
-        nstk = 0;
-      } else {
-        colour_store(ka.col, slot, L_r, L_g, L_b);
-      }
+      colour_store(ka.col, slot, L_r, L_g, L_b);
       in_path = false;
     }
     YK_STAMP(5);
@@ -2837,7 +2790,6 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.w_sh = wa.w_sh;
   ka.pad_n = 0;
   ReduceArgs ra;
-  ra.mat = ctx->d_mat;
   ra.acc = ctx->d_acc;
   ra.order = ctx->d_order;
   ra.rgb = rgb_dev;
