@@ -55,8 +55,8 @@ enum { YK_MATERIAL_LAMBERTIAN = 0, YK_MATERIAL_METAL = 1, YK_MATERIAL_DIELECTRIC
  * pinned against the reference's headers with the literals written as T(...): DESIGN.md §2.)
  * FP32 has its own BVH, whose boxes and per-ray cone carry the float sphere test's proven error
  * (DESIGN.md §4.1): its images equal the linear scan's bit for bit.
- * FP32 is a PARITY mode, not a speed mode: it reproduces render<float>'s images, and it is ~10%
- * SLOWER than FP64 on this chip (1920x1080x512: ~190 vs ~171 ms).  render<float>'s paths bounce
+ * FP32 is a PARITY mode, not a speed mode: it reproduces render<float>'s images, and it is ~15%
+ * SLOWER than FP64 on this chip (1920x1080x512: ~191 vs ~163 ms).  render<float>'s paths bounce
  * 7% more (its float sphere test), its tree needs the cone's extra plane read and wider boxes,
  * and the FP64 arithmetic the float path saves was not what bound the kernel.
  * Use FP64 (or xor128, the fast mode) for speed. */
