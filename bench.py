@@ -87,6 +87,33 @@ def pmc_facts(workload=None):
 
 
 PMC_LANE_OPS = os.path.join(ROOT, "profiles", "pmc_lane_ops.json")
+PMC_HBM = os.path.join(ROOT, "profiles", "pmc_hbm.json")
+HBM_MEASURED_GBPS = 6290.0    # MI355X_MICROARCH.md chip table: float4 copy, measured
+
+
+def hbm_measured(samples_per_step, ms_per_step, alg_bytes_per_sample, path=PMC_HBM):
+    """The step's HBM traffic from the PMC counters (north_star "rocprof
+    achieved-HBM-GB/s against the chip's peak"): every kernel of a launch — render, warm-up,
+    reduce — in bytes per sample (tools/pmc_hbm.py over tools/pmc_profile.sh's FETCH_SIZE and
+    WRITE_SIZE passes of the same build), times the step's samples over the step's time.  None
+    without the committed summary."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f)
+    bps = rec["bytes_per_sample"]
+    gbps = bps * samples_per_step / (ms_per_step * 1e-3) / 1e9
+    return {
+        "achieved": round(gbps, 2), "unit": "GB/s",
+        "peak": HBM_PEAK_GBPS, "frac": round(gbps / HBM_PEAK_GBPS, 5),
+        "peak_measured": HBM_MEASURED_GBPS, "frac_of_measured": round(gbps / HBM_MEASURED_GBPS, 5),
+        "bytes_per_sample": round(bps, 3),
+        "bytes_per_sample_by_kernel": {k: round(v["bytes_per_sample"], 3) for k, v in rec["kernels"].items()},
+        "traffic_per_step": round(bps * samples_per_step),
+        "traffic_over_algorithmic": round(bps / alg_bytes_per_sample, 1),
+        "source": f"{os.path.relpath(path, ROOT)} ({rec['source']}); GB/s = bytes per sample x the "
+                  f"step's samples / ms_per_step",
+    }
 
 
 def pmc_lane_ops():
@@ -98,19 +125,55 @@ def pmc_lane_ops():
         return json.load(f)
 
 
-def reference_calibration(seed0, W=160, spp=32, depth=50):
-    """The reference's own loop beside the port on this host (north_star: "the
-    reference CPU loop timed on the node's own host cores").  oracle/_ref/ref_harness is the
-    reference's headers (ray_color, hittable_list, sphere, mt19937, generate_canonical, math::sqrt)
-    and its per-pixel loop with the constexpr seed, -O2, one thread (oracle/Makefile; built only
-    where /root/reference exists, the binary travels with the tree).  The 485-sphere scene does
-    not compile through the reference's tuple API, so it renders the reference's own
-    4-sphere world (source.cpp:103-112) and the 48-sphere slice of the final scene
-    (tests/golden/final48.yks, through the harness's scene-file tuple); the port
-    (oracle/yk_oracle.c) renders the same pixels on one thread, and both images are compared."""
+def _run_harness(harness, mode, arg, W, H, spp, depth, seed0, nproc, timeout_s):
+    """oracle/_ref/ref_harness as `nproc` processes over interleaved rows (YK_REF_ROWS = k:nproc,
+    row y → process y mod nproc), the image assembled from their row sets; wall clock from the
+    first start to the last exit.  Raises on a non-zero exit or on the time limit (every process
+    is killed first)."""
     import subprocess
     import tempfile
 
+    import numpy as np
+    with tempfile.TemporaryDirectory() as td:
+        paths = [os.path.join(td, f"h{k}.rgb") for k in range(nproc)]
+        t = time.perf_counter()
+        procs = [subprocess.Popen([harness, mode, arg, str(W), str(H), str(spp), str(depth), str(seed0), paths[k]],
+                                  env=dict(os.environ, YK_REF_ROWS=f"{k}:{nproc}"),
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+                 for k in range(nproc)]
+        try:
+            for pr in procs:
+                left = max(0.1, timeout_s - (time.perf_counter() - t))
+                _, err = pr.communicate(timeout=left)
+                if pr.returncode != 0:
+                    raise RuntimeError(f"ref_harness exit {pr.returncode}: {err.decode(errors='replace')[-300:]}")
+        finally:
+            for pr in procs:
+                if pr.poll() is None:
+                    pr.kill()
+                    pr.wait()
+        dt = time.perf_counter() - t
+        img = np.zeros((H, W, 3), np.uint8)
+        for k in range(nproc):
+            img[k::nproc] = np.fromfile(paths[k], np.uint8).reshape(H, W, 3)[k::nproc]
+    return img, dt
+
+
+def reference_calibration(seed0, nthreads, W=160, spp=32, depth=50, W_all=640, timeout_s=120.0):
+    """The reference's own loop beside the port on this host (north_star: "the reference CPU loop
+    timed on the node's own host cores ... core count stated").  oracle/_ref/ref_harness is the
+    reference's headers (ray_color, hittable_list, sphere, mt19937, generate_canonical, math::sqrt)
+    and its per-pixel loop (source.cpp:122-172) with the constexpr seed, -O2 (oracle/Makefile;
+    built only where /root/reference exists, the binary travels with the tree).  The 485-sphere
+    scene does not compile through the reference's tuple API, so it renders the
+    reference's own 4-sphere world (source.cpp:103-112) and the 48-sphere slice of the final scene
+    (tests/golden/final48.yks, through the harness's scene-file tuple).
+      one_core:  W x H x spp on one thread each, harness and port (oracle/yk_oracle.c);
+      all_cores: W_all x H x spp with the harness as `nthreads` processes over interleaved rows
+                 (the reference's own `par` mode does not run, source.cpp:17-19,85-96, SURVEY
+                 finding 8) and the port on `nthreads` threads.
+    Both images are compared; a failure or a time-out is recorded, never raised (a side
+    measurement must not cost the bench line)."""
     import numpy as np
 
     import golden_data
@@ -120,27 +183,42 @@ def reference_calibration(seed0, W=160, spp=32, depth=50):
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if not os.path.exists(harness):
         return {"skipped": "oracle/_ref/ref_harness absent (built from /root/reference by oracle/Makefile)"}
-    H = image_height_for(W)
-    out = {"method": f"{W}x{H}x{spp}, depth {depth}, seed0 {seed0}, one thread each, wall clock; "
-                     "harness = the reference's headers and loop (-O2), port = oracle/yk_oracle.c (-O2)"}
     final48 = os.path.join(ROOT, "tests", "golden", "final48.yks")
-    for name, mode, arg, scene in (("ref4", "render", "ref4", (refscenes.ref4(), refscenes.reference_camera())),
-                                   ("final48", "render_file", final48, golden_data.read_scene_file(final48))):
-        with tempfile.TemporaryDirectory() as td:
-            rgb_path = os.path.join(td, "h.rgb")
-            t = time.perf_counter()
-            subprocess.run([harness, mode, arg, str(W), str(H), str(spp), str(depth), str(seed0), rgb_path],
-                           check=True, stdout=subprocess.DEVNULL)
-            dt_h = time.perf_counter() - t
-            h_rgb = np.fromfile(rgb_path, np.uint8).reshape(H, W, 3)
-        t = time.perf_counter()
-        p_rgb, _, _, _ = oracle_lib.render(scene[0], scene[1], make_params(W, H, spp, depth, seed0), nthreads=1)
-        dt_p = time.perf_counter() - t
-        n = W * H * spp
-        out[name] = {"spheres": len(scene[0]), "harness_msps": round(n / dt_h / 1e6, 4),
-                     "port_msps": round(n / dt_p / 1e6, 4), "port_over_harness": round(dt_h / dt_p, 3),
-                     "harness_s": round(dt_h, 2), "port_s": round(dt_p, 2),
-                     "images_equal": bool((h_rgb == p_rgb).all())}
+    scenes = (("ref4", "render", "ref4", lambda: (refscenes.ref4(), refscenes.reference_camera())),
+              ("final48", "render_file", final48, lambda: golden_data.read_scene_file(final48)))
+    out = {"method": f"one_core: {W}x{image_height_for(W)}x{spp}, one thread each; all_cores: "
+                     f"{W_all}x{image_height_for(W_all)}x{spp}, the harness as {nthreads} processes over "
+                     f"interleaved rows, the port on {nthreads} threads; depth {depth}, seed0 {seed0}, wall "
+                     f"clock; harness = the reference's headers and loop (-O2), port = oracle/yk_oracle.c (-O2)",
+           "cores": nthreads}
+    mismatch = []
+    for leg, w, nt in (("one_core", W, 1), ("all_cores", W_all, nthreads)):
+        h = image_height_for(w)
+        n = w * h * spp
+        res = {}
+        for name, mode, arg, scene_fn in scenes:
+            try:
+                scene = scene_fn()
+                h_rgb, dt_h = _run_harness(harness, mode, arg, w, h, spp, depth, seed0, nt, timeout_s)
+                t = time.perf_counter()
+                p_rgb, _, _, _ = oracle_lib.render(scene[0], scene[1], make_params(w, h, spp, depth, seed0),
+                                                   nthreads=nt)
+                dt_p = time.perf_counter() - t
+                eq = bool((h_rgb == p_rgb).all())
+                if not eq:
+                    mismatch.append(f"{leg}/{name}")
+                res[name] = {"spheres": len(scene[0]), "harness_msps": round(n / dt_h / 1e6, 4),
+                             "port_msps": round(n / dt_p / 1e6, 4), "port_over_harness": round(dt_h / dt_p, 3),
+                             "harness_s": round(dt_h, 2), "port_s": round(dt_p, 2), "images_equal": eq}
+            except Exception as e:  # noqa: BLE001 (recorded, never fatal)
+                res[name] = {"error": f"{type(e).__name__}: {e}"[:400]}
+        out[leg] = res
+    fin = out["all_cores"].get("final48", {})
+    if "harness_msps" in fin:
+        out["harness_msps_all_cores"] = fin["harness_msps"]
+    out["images_equal"] = not mismatch
+    if mismatch:
+        out["IMAGES_DIFFER"] = mismatch
     return out
 
 
@@ -523,17 +601,21 @@ def main():
             },
             "issue": issue,
             "hbm": {"algorithmic_bytes_per_launch": round(hbm_step / launches),
-                    "achieved": round(hbm_gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(hbm_gbps / HBM_PEAK_GBPS, 7), "traffic": traffic,
-                    "traffic_per_sample": round(traffic_ps, 3) if traffic_ps else None,
+                    "algorithmic_achieved": round(hbm_gbps, 4), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "algorithmic_frac": round(hbm_gbps / HBM_PEAK_GBPS, 7),
+                    # the whole step's PMC-measured traffic (render + warm-up + reduce) as GB/s
+                    "measured": hbm_measured(pix_mine * spp, ms_per_step, alg_ps),
+                    "render_kernel_traffic_per_launch": traffic,
+                    "render_kernel_traffic_per_sample": round(traffic_ps, 3) if traffic_ps else None,
                     "algorithmic_bytes_per_sample": round(alg_ps, 4),
-                    "traffic_over_algorithmic": round(traffic_ps / alg_ps, 1) if traffic_ps else None,
+                    "render_kernel_traffic_over_algorithmic": round(traffic_ps / alg_ps, 1) if traffic_ps else None,
                     "device_bytes": tst["device_bytes"], "call_bytes": tst["call_bytes"],
                     "algorithmic": f"SURVEY §8(d): the RGB8 image ({pix_mine * 3} B) once per "
                                    f"step + the scene ({scene_bytes} B) once per workgroup "
-                                   f"({tst['grid_blocks']} per launch); traffic = PMC FETCH_SIZE x2 + "
-                                   f"WRITE_SIZE per launch (scratch: the start records, the colour "
-                                   f"records, the processing order, MT fallback state)"},
+                                   f"({tst['grid_blocks']} per launch); render_kernel_traffic = PMC FETCH_SIZE "
+                                   f"x2 + WRITE_SIZE of yk_render_persistent alone (scratch: the start "
+                                   f"records, the colour records, MT fallback state); `measured` adds "
+                                   f"the warm-up and reduce kernels: the step's traffic"},
             # the union of the step's render spans can exceed the step (a step's first renders are
             # enqueued while the previous step's still run): then launch_ms is the step / launches
             "launch_ms_unclamped": round(busy_ms / launches, 4),
@@ -602,7 +684,17 @@ def main():
                           f"{dta:.1f} s; a random_device seed per sample as in the runtime build "
                           f"(source.cpp:159), so not reproducible"},
         }
-        result["cpu_baseline"]["reference_calibration"] = reference_calibration(args.seed0)
+        cal = reference_calibration(args.seed0, nthreads)
+        result["cpu_baseline"]["reference_calibration"] = cal
+        fin = cal.get("all_cores", {}).get("final48", {})
+        if "harness_msps" in fin:
+            # the reference's own loop on every usable core (the 48-sphere slice: the 485-sphere
+            # scene does not compile through its tuple API), beside the port on the same cores
+            result["cpu_baseline"]["variants"]["reference_loop_all_cores"] = {
+                "value": fin["harness_msps"], "cores": nthreads, "kind": "reference",
+                "port_same_cores_same_scene": fin["port_msps"],
+                "port_over_reference": fin["port_over_harness"], "images_equal": fin["images_equal"],
+                "sample": cal["method"].split("; all_cores: ")[1].split(";")[0] + ", tests/golden/final48.yks"}
         result["parity_vs_cpu"] = {
             "rows_compared": len(rows),
             "rmse": float(np.sqrt(np.mean(diff ** 2))),

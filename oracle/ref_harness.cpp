@@ -31,6 +31,7 @@
 //     the rays printed by the reference's ray_color itself (the -l 3 fixture)
 //   render_file / samples_file (and the 32 / _x128 forms): <scene> is a scene file of 5, 24 or 48
 //     spheres (configs 2-5 content: dielectric, fuzzed metal, thin-lens camera; see below)
+#include <algorithm>
 #include <cmath>
 #include <iomanip>
 #include <iostream>
@@ -318,7 +319,16 @@ template <class T, class E, class World, class Cam>
 int render(const World& world, const Cam& cam, const job& j, const char* out_rgb, const char* out_sums) {
   std::vector<unsigned char> rgb(std::size_t(j.W) * j.H * 3);
   std::vector<double> sums(std::size_t(j.W) * j.H * 3);
-  for (std::uint32_t y = 0; y < j.H; ++y) {
+  // YK_REF_ROWS="b:k" renders rows b, b + k, b + 2k, ... only (the others stay 0): k processes of
+  // this loop then cover the image on k cores (bench.py reference_calibration; the reference's
+  // own par mode, source.cpp:85-96, does not run)
+  std::uint32_t y0 = 0, ystep = 1;
+  if (const char* e = std::getenv("YK_REF_ROWS")) {
+    char* rest = nullptr;
+    y0 = std::strtoul(e, &rest, 10);
+    if (rest && *rest == ':') ystep = std::max(1ul, std::strtoul(rest + 1, nullptr, 10));
+  }
+  for (std::uint32_t y = y0; y < j.H; y += ystep) {
     for (std::uint32_t x = 0; x < j.W; ++x) {
       auto iota = std::views::iota(0u, j.spp);
       yk::color3d pc = std::transform_reduce(

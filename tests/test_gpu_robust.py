@@ -91,3 +91,55 @@ def test_config5_frame_on_a_device_short_of_memory():
     q = make_params(1920, 1080, 4096, 200, 404, rows=(rows[0], 2, rows[1] - rows[0]))
     _, want, _, _ = oracle_lib.render(arr, cam, q, nthreads=16, want_rgb=False, want_sums=True)
     assert got[list(rows)].tobytes() == want.tobytes()
+
+
+_RETRY_CODE = r'''
+import hashlib, json, os, sys
+sys.path.insert(0, os.environ["YK_ROOT"])
+import torch
+import uecraytracing_amd as yk
+from uecraytracing_amd.records import make_params
+arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
+out = {}
+with yk.Renderer(0) as r:
+    r.set_scene(arr, cam)
+    for spp in (32, 40):  # synced 4, 8, 20 and 4, 8, 16, 12: launches up to 2048 slots per warm-up wave
+        img = r.render(make_params(1920, 1080, spp, 50, 404))
+        st = r.stats()
+        out[str(spp)] = {"sha": hashlib.sha256(img.tobytes()).hexdigest(), "rows": img[[7, 1071]].tolist(),
+                         "call_bytes": st["call_bytes"], "launches": st["launches"]}
+print(json.dumps(out))
+'''
+
+
+def test_lens_retry_ring_fallbacks_are_bit_exact():
+    """ADVICE r5: the deferred lens-retry warm-up's two fallbacks, forced by test builds of the
+    library (uecraytracing_amd/csrc/Makefile TESTVARIANTS, -DYK_RETRY_CAP_FORCE): a ring of 64
+    records per wave against ~440 expected rejections per wave at the frame's 2048 slots per
+    warm-up wave, so it fills and the samples that find it full reach the render as kNoStart starts
+    the render makes itself; and no ring (0), the in-line rejection loop a failed ring allocation
+    falls back to.  The thin-lens final scene at 1920x1080: both images equal the product
+    library's byte for byte and two rows equal the CPU oracle's; the ring's bytes show in
+    call_bytes (product > 64-record ring > none)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = yk.LIB_DIR  # uecraytracing_amd/lib
+    repo = os.path.dirname(os.path.dirname(root))
+    res = {}
+    for name, lib in (("product", os.path.join(root, "libykgpu.so")), ("retry64", os.path.join(root, "abl", "libykgpu_retry64.so")),
+                      ("retry0", os.path.join(root, "abl", "libykgpu_retry0.so"))):
+        assert os.path.exists(lib), f"{lib}: built by uecraytracing_amd/csrc/Makefile (all)"
+        env = dict(os.environ, YKGPU_LIB_OVERRIDE=lib, YK_ROOT=repo)
+        pr = subprocess.run([sys.executable, "-c", _RETRY_CODE], env=env, capture_output=True, text=True,
+                            timeout=240)
+        assert pr.returncode == 0, pr.stderr[-2000:]
+        res[name] = json.loads([ln for ln in pr.stdout.splitlines() if ln.startswith("{")][-1])
+    arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
+    for spp in ("32", "40"):
+        assert res["retry64"][spp]["sha"] == res["product"][spp]["sha"]
+        assert res["retry0"][spp]["sha"] == res["product"][spp]["sha"]
+        assert res["product"][spp]["call_bytes"] > res["retry64"][spp]["call_bytes"] > res["retry0"][spp]["call_bytes"]
+    want, _, _, _ = oracle_lib.render(arr, cam, make_params(1920, 1080, 32, 50, 404, rows=(7, 2, 1064)))
+    np.testing.assert_array_equal(np.array(res["retry64"]["32"]["rows"], dtype=np.uint8), want)

@@ -180,6 +180,45 @@ def test_bench_line_carries_the_lane_op_roofline():
     per_step = vo["render"]["algorithmic"] * b["roofline"]["launches_per_step"] + \
         vo["warmup"]["algorithmic"] * b["roofline"]["launches_per_step"]
     assert abs(per_step / vo["step"]["algorithmic"] - 1) < 0.01
-    if b["roofline"]["hbm"].get("traffic_per_sample"):
-        h = b["roofline"]["hbm"]
-        assert abs(h["traffic_per_sample"] / h["algorithmic_bytes_per_sample"] / h["traffic_over_algorithmic"] - 1) < 0.01
+    h = b["roofline"]["hbm"]
+    tps = h.get("render_kernel_traffic_per_sample", h.get("traffic_per_sample"))
+    if tps:
+        r = h.get("render_kernel_traffic_over_algorithmic", h.get("traffic_over_algorithmic"))
+        assert abs(tps / h["algorithmic_bytes_per_sample"] / r - 1) < 0.01
+
+
+def test_measured_hbm_covers_every_kernel_of_the_step():
+    """profiles/pmc_hbm.json (tools/pmc_hbm.py): the render kernel's bytes per
+    sample are the render summary's of the same PMC run, the step's figure is the sum over render,
+    warm-up and reduce, and the bench line's `hbm.measured` recomputes from it: bytes per sample x
+    the step's samples / ms_per_step, its fractions of the 8 TB/s spec and the 6.29 TB/s measured
+    copy rate."""
+    import bench
+    f = os.path.join(PROF, "pmc_hbm.json")
+    if not os.path.exists(f):
+        pytest.skip("no per-kernel HBM summary in profiles/")
+    rec = json.load(open(f))
+    ks = rec["kernels"]
+    assert set(ks) == {"render", "warmup", "reduce"}
+    assert abs(sum(k["bytes_per_sample"] for k in ks.values()) - rec["bytes_per_sample"]) < 1e-6
+    tag = rec["source"].split("gpurun_out/")[1].split("/")[0]
+    summ = os.path.join(PROF, f"{tag}_pmc_summary.json")
+    if os.path.exists(summ):
+        r = json.load(open(summ))["hbm_bytes_per_sample"]
+        assert abs(ks["render"]["bytes_per_sample"] / r - 1) < 1e-3
+    # a launch's scratch round trip: the warm-up writes each sample's 64-B start record, the
+    # render reads it and writes a 32-B colour record, the reduce reads that
+    assert ks["warmup"]["write_bytes_per_sample"] > 64 and ks["render"]["fetch_bytes_per_sample"] > 64
+    assert ks["render"]["write_bytes_per_sample"] > 32 and ks["reduce"]["fetch_bytes_per_sample"] > 32
+    m = bench.hbm_measured(1000, 2.0, 0.5, f)
+    assert abs(m["achieved"] - rec["bytes_per_sample"] * 1000 / 2e-3 / 1e9) < 0.01
+    assert abs(m["frac"] - m["achieved"] / bench.HBM_PEAK_GBPS) < 1e-4
+    assert abs(m["frac_of_measured"] - m["achieved"] / bench.HBM_MEASURED_GBPS) < 1e-4
+    b = json.load(open(latest_bench()))
+    bm = b["roofline"]["hbm"].get("measured")
+    if bm:
+        spp = b["config"]["spp"]
+        W, H = (int(x) for x in b["config"]["image"].split("x"))
+        want = bm["bytes_per_sample"] * W * H * spp / b["n_gpus"] / (b["ms_per_step"] * 1e-3) / 1e9
+        assert abs(bm["achieved"] / want - 1) < 0.01
+        assert 0 < bm["frac"] < 1

@@ -159,8 +159,11 @@ def test_rank_tile_refuses_an_empty_tile():
     column set, which the C-ABI reads as 'every column' (col_count 0) and rejects; rank_tile says
     so up front, naming the row dealing, which still works for such an image."""
     from uecraytracing_amd.tiles import rank_tile
-    with pytest.raises(ValueError, match="deal rows"):
+    with pytest.raises(ValueError, match="deal rows") as e:
         rank_tile(7, 8, 40, 56, "cols")
+    assert "width > 56 needed" in str(e.value)  # ADVICE r5: the real bound, one band per rank
+    # 57 columns over 8 ranks: the last rank's band is one column wide, every rank gets pixels
+    assert rank_tile(7, 8, 40, 57, "cols")["cols"] == (56, 1, 8, 3)
     assert rank_tile(6, 8, 40, 56, "cols")["cols"] == (48, 8, 8, 3)
     assert rank_tile(7, 8, 40, 56, "rows")["rows"] == (7, 5, 8, 0)
     with pytest.raises(ValueError, match="rank 5 would get none"):

@@ -11,5 +11,7 @@ cp $S/kt/run_kernel_stats.csv $P/${T}_kernel_stats.csv
 python3 tools/kernel_union.py $S/kt/run_kernel_trace.csv "yk_render_persistent<true, 0>" $P/${T}_kernel_union.json 1536 32 > /dev/null
 cp $S/pmc_summary.json $P/${T}_pmc_summary.json
 cp $S/pmc_summary.json $P/pmc_summary.json
+[ -f $S/pmc_summary_warmup.json ] && cp $S/pmc_summary_warmup.json $P/${T}_pmc_summary_warmup.json
+[ -f $S/pmc_hbm.json ] && cp $S/pmc_hbm.json $P/${T}_pmc_hbm.json && cp $S/pmc_hbm.json $P/pmc_hbm.json
 [ -f $S/gpu_tests.log ] && grep -E "PASSED|FAILED|SKIPPED|ERROR|passed|failed" $S/gpu_tests.log > $P/${T}_gpu_tests.txt || true
 ls -la $P/${T}_*

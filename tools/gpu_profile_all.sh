@@ -11,7 +11,9 @@ bash tools/pmc_profile.sh gpurun_out/$T/pmc || { echo PMC_FAILED; exit 3; }
 # (pmc_profile.sh runs bench.py --steps 1 --warmup 1 per pass: two 1920x1080x512 calls)
 python3 tools/pmc_summary.py gpurun_out/$T/pmc "yk_render_persistent<true, 0>" final42_1920x1080x512_d50_n1 gpurun_out/$T/pmc_summary.json 2123366400 > /dev/null || exit 4
 python3 tools/pmc_summary.py gpurun_out/$T/pmc "yk_mt_warmup" final42_1920x1080x512_d50_n1 gpurun_out/$T/pmc_summary_warmup.json > /dev/null || exit 4
+python3 tools/pmc_hbm.py gpurun_out/$T/pmc 1061683200 19 gpurun_out/$T/pmc_hbm.json > /dev/null || exit 4
 cp gpurun_out/$T/pmc_summary.json profiles/pmc_summary.json
+cp gpurun_out/$T/pmc_hbm.json profiles/pmc_hbm.json
 timeout -k 10 400 python bench.py > gpurun_out/$T/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/$T/bench.log; exit 1; }
 grep '^{' gpurun_out/$T/bench.log | tail -1 > gpurun_out/$T/bench.json
 cat gpurun_out/$T/bench.json

@@ -2679,6 +2679,16 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     for (const auto& l : sched)
       if (wave_slots((uint64_t)nps * l.second) <= kDeferSlots)
         retry_cap = std::max(retry_cap, retry_cap_for(wave_slots((uint64_t)nps * l.second)));
+  // a call whose launches were shrunk for want of memory runs the rejection loop in line: the
+  // shrink loop above budgets the start-record and colour rings only, so the plan it settled on
+  // is the plan the call runs (no ring allocated afterwards out of the reserve it kept)
+  if (mem_shrinks) retry_cap = 0;
+#ifdef YK_RETRY_CAP_FORCE
+  // (test variants, tests/test_gpu_robust.py): the ring's capacity forced so that its fallbacks
+  // run — 64 records per wave fill up (the samples that find it full reach the render as kNoStart
+  // starts it makes itself), 0 is the in-line loop a failed ring allocation falls back to
+  if (retry_cap) retry_cap = YK_RETRY_CAP_FORCE;
+#endif
   size_t retry_n = (size_t)ctx->cus * warm_per_cu(false) * 4u * retry_cap * 3u;
   if (retry_cap && (rc = grow(ctx->d_retry, ctx->retry_cap, retry_n, sizeof(uint4)))) {
     if (rc != YK_ERR_NOMEM) return rc;
@@ -3655,6 +3665,9 @@ int ykgpu_group_render(ykgpu_group* g, const yk_render_params* p, uint8_t* rgb_h
     tot.device_bytes += s.device_bytes + g->tile_cap[e];
     tot.call_bytes += s.call_bytes + rows[e] * row_bytes;
     tot.sclk_mhz = std::max(tot.sclk_mhz, s.sclk_mhz);
+    // (ABI 11) the largest launch of any entry, and every entry's memory-pressure shrinks
+    tot.launch_spp = std::max(tot.launch_spp, s.launch_spp);
+    tot.mem_shrinks += s.mem_shrinks;
   }
   tot.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   g->total = tot;

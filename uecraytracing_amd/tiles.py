@@ -73,7 +73,7 @@ def rank_tile(rank: int, world: int, height: int, width: int, deal: str = DEAL) 
     """make_params keyword arguments (rows=, cols=) of rank's tile under `deal` ("rows" or
     "cols").  Every rank must get pixels: the C-ABI takes no empty row or column set (col_count
     0 means every column), so an image too small for the split — fewer than 8 x world columns
-    dealt in 8-column bands, fewer than world rows — is refused here, naming the other dealing."""
+    dealt in 8-column bands, i.e. width <= 8 (world - 1), fewer than world rows — is refused here, naming the other dealing."""
     if deal == "rows":
         rows = tile_rows(rank, world, height)
         if rows[1] == 0:
@@ -83,8 +83,8 @@ def rank_tile(rank: int, world: int, height: int, width: int, deal: str = DEAL) 
         cols = tile_cols(rank, world, width) if world > 1 else None
         if cols is not None and cols[1] == 0:
             raise ValueError(f"{width} columns in {1 << COL_BAND_LOG2}-column bands cannot be dealt over {world} "
-                             f"ranks (rank {rank} would get none; width >= {world << COL_BAND_LOG2} needed): "
-                             "deal rows instead")
+                             f"ranks (rank {rank} would get none; every rank needs at least one band: width > "
+                             f"{(world - 1) << COL_BAND_LOG2} needed): deal rows instead")
         return {"rows": (0, height, 1, 0), "cols": cols}
     raise ValueError(f"deal must be 'rows' or 'cols', not {deal!r}")
 
