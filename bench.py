@@ -302,51 +302,70 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf, deal):
     return out
 
 
-def rank_tiles(ren, stream, seed0, frame_ms, deal):
+def rank_tiles(ren, stream, seed0, frame, deal, steps, warmup):
     """The N-GPU bound on this GPU: every rank's tile of the N-way
-    split under `deal` (8-column bands or single rows, tiles.py) rendered ALONE (ms per call over 4
-    back-to-back calls after a warm one, HIP events on the bench stream: the per-rank steps of the
-    N-GPU bench), for config 3 at N = 2, 4, 8 and config 4's eight tiles, and the other dealing at
-    N = 8 for comparison.  The slowest tile bounds the N-GPU step before the gather;
-    `speedup_bound` = the single-GPU frame (the contract line's ms per step for config 3; the
-    same back-to-back timing of whole config-4 frames) / the slowest tile."""
+    split under `deal` (8-column bands or single rows, tiles.py) rendered ALONE, timed exactly as
+    the contract loop times the frame — `warmup` untimed calls, a synchronisation, then `steps`
+    calls back to back (HIP events on the bench stream) — for config 3 at N = 2, 4, 8 and config
+    4's eight tiles, and the other dealing at N = 8 for comparison.  Like with like: the first
+    timed call starts synced (its launches ramp up) and the rest start while the
+    previous call still runs, in the frame's steps and in the tiles' alike; a tile timed over fewer
+    calls than the frame would carry a larger share of that first call (VERDICT r5's 1.086 was 4
+    tile calls against 20 frame steps; profiles/r06b).  The slowest tile bounds the N-GPU step
+    before the gather; `speedup_bound` = the single-GPU frame / the slowest tile.  `in_flight`
+    figures leave the first call out (ms per call between the ends of calls 1 and K).
+    frame: {"ms", "in_flight_ms"} of the contract loop (config 3)."""
     import torch
 
     import uecraytracing_amd as yk
     from uecraytracing_amd.records import image_height_for, make_params
     from uecraytracing_amd.tiles import rank_tile
 
-    def call_ms(p, out, calls=4):
-        # one warm call, then `calls` back-to-back calls as the N-GPU bench's steps issue them (a
-        # call's first launches overlap the previous call's last, DESIGN §3): ms per call
+    def call_ms(p, out, calls):
+        # the contract loop's structure: warm-up calls, a sync, `calls` back-to-back calls; an
+        # event on the stream after each call fires when that call's image is complete
         with torch.cuda.stream(stream):
-            ren.render_async(p, out.data_ptr(), stream.cuda_stream)
-        torch.cuda.synchronize()
-        with torch.cuda.stream(stream):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(calls):
+            for _ in range(max(1, warmup)):
                 ren.render_async(p, out.data_ptr(), stream.cuda_stream)
-            e1.record(stream)
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / calls
+        with torch.cuda.stream(stream):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(calls + 1)]
+            ev[0].record(stream)
+            for k in range(calls):
+                ren.render_async(p, out.data_ptr(), stream.cuda_stream)
+                ev[k + 1].record(stream)
+        torch.cuda.synchronize()
+        total = ev[0].elapsed_time(ev[calls]) / calls
+        inflight = ev[1].elapsed_time(ev[calls]) / (calls - 1) if calls > 1 else total
+        return total, inflight
 
-    out = {"deal": deal}
+    out = {"deal": deal, "steps": steps, "warmup": warmup,
+           "method": "per tile: `warmup` calls, a sync, `steps` back-to-back calls (the contract loop's "
+                     "structure); ms per call; in_flight = calls 2..K"}
     other = "rows" if deal == "cols" else "cols"
     for cfg, W, spp, ns in (("config3", 1920, 512, (2, 4, 8)), ("config4", 3840, 1024, (8,))):
         spheres, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
         ren.set_scene(spheres, cam)
         H = image_height_for(W)
+        # config 4's frame takes ~1.3 s per call: at most 6 calls for it and its tiles alike
+        k = steps if cfg == "config3" else min(steps, 6)
         buf = torch.empty((H, W, 3), dtype=torch.uint8, device=torch.device("cuda", ren.device))
-        full = frame_ms if cfg == "config3" else call_ms(make_params(W, H, spp, 50, seed0, flags=0), buf)
+        if cfg == "config3":
+            full, full_if = frame["ms"], frame["in_flight_ms"]
+        else:
+            full, full_if = call_ms(make_params(W, H, spp, 50, seed0, flags=0), buf, k)
         # the bench's dealing at every N; the other dealing at N = 8 for comparison
         for n, d in [(n, deal) for n in ns] + [(8, other)]:
-            ms = [call_ms(make_params(W, H, spp, 50, seed0, flags=0, **rank_tile(r, n, H, W, d)), buf)
+            ms = [call_ms(make_params(W, H, spp, 50, seed0, flags=0, **rank_tile(r, n, H, W, d)), buf, k)
                   for r in range(n)]
+            tot = [m[0] for m in ms]
+            inf = [m[1] for m in ms]
             out[f"{cfg}_n{n}" + ("" if d == deal else f"_{d}")] = {
-                "tile_ms": [round(m, 3) for m in ms], "slowest_ms": round(max(ms), 3),
-                "frame_ms": round(full, 3), "speedup_bound": round(full / max(ms), 3),
-                "slowest_over_ideal": round(max(ms) / (full / n), 4)}
+                "calls": k, "tile_ms": [round(m, 3) for m in tot], "slowest_ms": round(max(tot), 3),
+                "frame_ms": round(full, 3), "speedup_bound": round(full / max(tot), 3),
+                "slowest_over_ideal": round(max(tot) / (full / n), 4),
+                "in_flight": {"tile_ms": [round(m, 3) for m in inf], "frame_ms": round(full_if, 3),
+                              "slowest_over_ideal": round(max(inf) / (full_if / n), 4)}}
     return out
 
 
@@ -468,6 +487,9 @@ def main():
         elapsed = float(t.item())
 
     call_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    # ms per step after the first (which starts synced): between the ends of steps 1
+    # and K on the bench stream (HIP events; e1 of a step fires when its image is complete)
+    step_in_flight_ms = (ev[0][1].elapsed_time(ev[-1][1]) / (len(ev) - 1)) if len(ev) > 1 else call_ms
     tst = ren.stats()  # per-kernel event timings of the last timed step (same stream)
     launches = max(1, tst["launches"])
     # work counters: one more launch of the same workload with the counting instance, after the
@@ -567,6 +589,7 @@ def main():
                          + ("RCCL gather to rank 0" if backend == "nccl" else
                             f"{backend} gather to rank 0 through the host (rehearsal: ranks share a GPU)"),
         },
+        "ms_per_step_in_flight": round(step_in_flight_ms, 3),
         "scene_upload_ms": round(scene_upload_ms, 3),
         "value_incl_scene_upload": round(total_samples * args.steps
                                          / (elapsed + args.steps * scene_upload_ms * 1e-3) / 1e6, 3),
@@ -726,7 +749,8 @@ def main():
                                           args.deal)
 
     if rank == 0 and world == 1 and not args.no_tiles and (W, spp, depth, args.scene) == (1920, 512, 50, "final"):
-        result["tiles"] = rank_tiles(ren, stream, args.seed0, ms_per_step, args.deal)
+        result["tiles"] = rank_tiles(ren, stream, args.seed0, {"ms": ms_per_step, "in_flight_ms": step_in_flight_ms},
+                                     args.deal, args.steps, args.warmup)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

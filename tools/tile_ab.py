@@ -2,7 +2,8 @@
 call, then `calls` back-to-back render_async calls, ms per call (HIP events), two interleaved
 rounds, one subprocess per variant run (variants as tools/abtime.py: base or
 lib/abl/libykgpu_<name>.so, "@VAR=value" settings).  TILE="W:spp:N:rank:deal" (default the
-config-3 8-way tile "1920:512:8:0:cols"; N = 1 times the whole frame).
+config-3 8-way tile "1920:512:8:0:cols"; N = 1 times the whole frame; deal "rows3": rows in
+bands of 8).
 usage: [TILE=...] python tools/tile_ab.py <variant> [<variant> ...]"""
 import os
 import subprocess
@@ -18,10 +19,12 @@ from uecraytracing_amd.records import image_height_for, make_params
 from uecraytracing_amd.tiles import rank_tile
 W, spp, n, rank, deal = sys.argv[1].split(":")
 W, spp, n, rank = int(W), int(spp), int(n), int(rank)
+band = int(deal[4:]) if deal.startswith("rows") and len(deal) > 4 else None  # "rows3": 8-row bands
+deal = deal[:4]
 H = image_height_for(W)
 arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
 ren = yk.Renderer(0); ren.set_scene(arr, cam)
-p = make_params(W, H, spp, 50, 404, flags=0, **(rank_tile(rank, n, H, W, deal) if n > 1 else {}))
+p = make_params(W, H, spp, 50, 404, flags=0, **(rank_tile(rank, n, H, W, deal, band) if n > 1 else {}))
 buf = torch.empty((p.row_count, p.tile_width(), 3), dtype=torch.uint8, device="cuda:0")
 s = torch.cuda.Stream()
 calls = int(sys.argv[2])

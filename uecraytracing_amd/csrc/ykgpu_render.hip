@@ -2175,6 +2175,7 @@ struct ykgpu_context {
   // a global launch counter that numbers the ring slots, the scratch parity and the render
   // stream across calls
   std::vector<hipEvent_t> lev_prev;
+  uint32_t lev_prev_used = 0;  // (events of the previous call in lev_prev: YKGPU_TIMELINE prints them)
   uint32_t prev_n = 0;
   // the previous call's ring and scratch geometry: a call overlaps it only when every field is
   // equal (launch() `ov`; equal slot offsets in every ring buffer and scratch slice)
@@ -2858,6 +2859,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // per launch: [0] warm-up start, [1] warm-up end (aux), [2] render start, [3] render end (st),
   // [4] reduce start, [5] reduce end (red); the previous call's stay in lev_prev
   std::swap(ctx->lev, ctx->lev_prev);
+  ctx->lev_prev_used = ctx->lev_used;
   while (ctx->lev.size() < 6ull * nlaunch) {
     hipEvent_t e;
     YK_HIP(hipEventCreate(&e));
@@ -3072,6 +3074,19 @@ int finish_stats(ykgpu_context* ctx) {
   }
   ctx->stats.sclk_mhz = real > 0 ? cyc / real * 100.0 : 0.0;
   if (std::getenv("YKGPU_TIMELINE")) {  // diagnostic: per-launch event times (ms from the call's start)
+    // the previous call's launches on the same clock (negative: before this call's start), so the
+    // handover between back-to-back calls shows
+    for (uint32_t k = 0; k + 5 < ctx->lev_prev_used && k + 5 < ctx->lev_prev.size(); k += 6) {
+      float t[6];
+      bool ok = true;
+      for (int q = 0; q < 6 && ok; ++q) ok = hipEventElapsedTime(&t[q], ctx->ev0, ctx->lev_prev[k + q]) == hipSuccess;
+      if (!ok) {
+        (void)hipGetLastError();
+        break;
+      }
+      std::fprintf(stderr, "prev   %u: warm %8.3f %8.3f  render %8.3f %8.3f  reduce %8.3f %8.3f\n", k / 6, t[0],
+                   t[1], t[2], t[3], t[4], t[5]);
+    }
     for (uint32_t k = 0; k + 5 < ctx->lev_used; k += 6) {
       float t[6];
       for (int q = 0; q < 6; ++q) YK_HIP(hipEventElapsedTime(&t[q], ctx->ev0, ctx->lev[k + q]));

@@ -69,18 +69,18 @@ def tile_image_cols(rank: int, world: int, width: int, band_log2: int = COL_BAND
     return tile_image_rows(rank, world, width, band_log2)
 
 
-def rank_tile(rank: int, world: int, height: int, width: int, deal: str = DEAL) -> dict:
+def rank_tile(rank: int, world: int, height: int, width: int, deal: str = DEAL, band_log2: int | None = None) -> dict:
     """make_params keyword arguments (rows=, cols=) of rank's tile under `deal` ("rows" or
     "cols").  Every rank must get pixels: the C-ABI takes no empty row or column set (col_count
     0 means every column), so an image too small for the split — fewer than 8 x world columns
     dealt in 8-column bands, i.e. width <= 8 (world - 1), fewer than world rows — is refused here, naming the other dealing."""
     if deal == "rows":
-        rows = tile_rows(rank, world, height)
+        rows = tile_rows(rank, world, height, BAND_LOG2 if band_log2 is None else band_log2)
         if rows[1] == 0:
             raise ValueError(f"{height} rows cannot be dealt over {world} ranks (rank {rank} would get none)")
         return {"rows": rows}
     if deal == "cols":
-        cols = tile_cols(rank, world, width) if world > 1 else None
+        cols = tile_cols(rank, world, width, COL_BAND_LOG2 if band_log2 is None else band_log2) if world > 1 else None
         if cols is not None and cols[1] == 0:
             raise ValueError(f"{width} columns in {1 << COL_BAND_LOG2}-column bands cannot be dealt over {world} "
                              f"ranks (rank {rank} would get none; every rank needs at least one band: width > "
