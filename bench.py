@@ -6,8 +6,8 @@ One STEP = one full render of the headline configuration (BASELINE config 3): 19
 the reference's arithmetic.  Inputs (scene, camera) are resident in HBM before the timed region;
 the output RGB8 image is produced in HBM (rank 0 holds the assembled image).
 
-N > 1 (one process per GPU, torchrun): the image's columns are dealt cyclically in 8-column bands
-(band b → rank b mod N, every row; `--deal rows`: single rows, row r → rank r mod N), each rank
+N > 1 (one process per GPU, torchrun): the image's rows are dealt cyclically (row r → rank r mod N;
+`--deal cols`: 8-column bands over every row, band b → rank b mod N), each rank
 renders its tile into device memory, and the tiles are gathered to rank 0 over RCCL
 (torch.distributed 'nccl') and de-interleaved on device — all inside the timed region.
 The total image is fixed, so this is STRONG scaling.
@@ -243,7 +243,7 @@ def other_configs(ren, stream, seed0, nthreads, peak_tf, deal):
     out = {}
     cases = (("config5", "glass", 1920, 4096, 200, None, (17, 1061)),
              ("config4_rank0_of_8", "final", 3840, 1024, 50, (0, 8),
-              (0, 134) if deal == "rows" else (0, 1079, 2159)))
+              (0, 134, 269) if deal == "rows" else (0, 1079, 2159)))
     for name, scene, W, spp, depth, split, cmp_rows in cases:
         scene_file = os.path.join(yk.SCENE_DIR, f"{scene}_seed42.yks")
         spheres, cam = yk.read_scene(scene_file)
@@ -390,7 +390,7 @@ def parse():
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the BASELINE config 4 / 5 measurements (rank 0, N=1)")
     ap.add_argument("--deal", choices=("cols", "rows"), default=None,
-                    help="N-GPU split: 8-column bands over every row (default, tiles.DEAL) or single rows")
+                    help="N-GPU split: single rows (default, tiles.DEAL) or 8-column bands over every row")
     ap.add_argument("--no-tiles", action="store_true",
                     help="skip the per-rank tile timings of the N-GPU splits (rank 0, N=1)")
     return ap.parse_args()
@@ -583,7 +583,8 @@ def main():
                         f"seed0 {args.seed0}, mt19937 + FP64 bit-exact",
             "image": f"{W}x{H}", "spp": spp, "max_depth": depth, "spheres": len(spheres),
             "scene_file": os.path.relpath(scene_file, ROOT) if scene_file else None,
-            "partition": (f"rows dealt cyclically in bands of {1 << BAND_LOG2}" if args.deal == "rows" else
+            "partition": ((f"rows dealt cyclically in bands of {1 << BAND_LOG2}" if BAND_LOG2 else
+                           "single rows dealt cyclically (row r -> rank r mod N)") if args.deal == "rows" else
                           f"columns dealt cyclically in bands of {1 << COL_BAND_LOG2} (every row)")
                          + f" over {world} GPU(s), "
                          + ("RCCL gather to rank 0" if backend == "nccl" else

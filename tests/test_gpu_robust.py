@@ -11,6 +11,8 @@
   another allocation, BASELINE config 5's whole frame (1920x1080x4096, depth 200, ~69 GB of rings
   at full launch size) renders with smaller launches, bit-exact against the CPU oracle.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -32,12 +34,13 @@ def ren():
 def test_alternating_precisions_with_colliding_start_buffers(ren):
     torch = pytest.importorskip("torch")
     ren.set_scene(refscenes.mixed12(), refscenes.reference_camera())
-    # synced schedules 4, 8, 16, 24 (K = 24, FP64: 64-B records) and 4, 8, 16, 32 (K = 32, FP32:
-    # 48-B records): 1536 bytes of start records per pixel slot and launch buffer in both
-    ps = [make_params(96, 54, 52, 50, 404), make_params(96, 54, 60, 50, 404, precision=PRECISION_FP32)] * 3
+    # launch buffers of kmax samples per pixel: 48 (FP64, 64-B records; synced schedule 4, 8, 16,
+    # 20) and 64 (FP32, 48-B records; 4, 8, 16, 36): 3072 bytes of start records per pixel slot and
+    # launch buffer in both, while the colour buffers' offsets differ
+    ps = [make_params(96, 54, 48, 50, 404), make_params(96, 54, 64, 50, 404, precision=PRECISION_FP32)] * 3
     want = [ren.render(p) for p in ps[:2]] * 3
     st = ren.stats()
-    assert st["launch_spp"] == 32 and st["launches"] == 4
+    assert st["launch_spp"] == 64 and st["launches"] == 4
     outs = [torch.zeros((p.row_count, p.tile_width(), 3), dtype=torch.uint8, device="cuda:0") for p in ps]
     torch.cuda.synchronize()
     stream = torch.cuda.Stream()
@@ -143,3 +146,37 @@ def test_lens_retry_ring_fallbacks_are_bit_exact():
         assert res["product"][spp]["call_bytes"] > res["retry64"][spp]["call_bytes"] > res["retry0"][spp]["call_bytes"]
     want, _, _, _ = oracle_lib.render(arr, cam, make_params(1920, 1080, 32, 50, 404, rows=(7, 2, 1064)))
     np.testing.assert_array_equal(np.array(res["retry64"]["32"]["rows"], dtype=np.uint8), want)
+
+
+def test_two_and_three_launch_calls_back_to_back():
+    """Calls of an 8-way column tile of 1920x1080 (259,200 pixels): 512 spp is two launches of 256
+    spp and 768 spp three (launches of ~2^26 slots), with launch buffers of kmax = 256
+    either way, so the rings (three start-record buffers, two colour buffers) are deeper than a
+    two-launch call and every call reuses buffers of the calls before it (ctx->gev, run_len).
+    Enqueued back to back in a mixed order, every image equals the synced render of its params,
+    and two rows equal the CPU oracle's."""
+    torch = pytest.importorskip("torch")
+    from uecraytracing_amd.tiles import rank_tile
+    arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
+    with yk.Renderer(0) as r:
+        r.set_scene(arr, cam)
+        tk = rank_tile(3, 8, 1080, 1920, "cols")
+        p2 = make_params(1920, 1080, 512, 50, 404, **tk)
+        p3 = make_params(1920, 1080, 768, 50, 404, **tk)
+        want = {512: r.render(p2), 768: r.render(p3)}
+        st = r.stats()
+        assert st["launch_spp"] == 256
+        seq = [p2, p2, p3, p2, p3, p3, p2]
+        outs = [torch.zeros((1080, p2.tile_width(), 3), dtype=torch.uint8, device="cuda:0") for _ in seq]
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        for p, o in zip(seq, outs):  # no synchronisation between the calls
+            r.render_async(p, o.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        st = r.stats()  # the last call's: in flight, two launches at kmax
+        assert st["launches"] == 2 and st["launch_spp"] == 256
+        for p, o in zip(seq, outs):
+            np.testing.assert_array_equal(o.cpu().numpy(), want[p.samples_per_pixel])
+    xs = [x for x in range(1920) if (x >> 3) % 8 == 3]
+    cpu, _, _, _ = oracle_lib.render(arr, cam, make_params(1920, 1080, 512, 50, 404, rows=(5, 2, 1070)), nthreads=16)
+    np.testing.assert_array_equal(want[512][[5, 1075]], cpu[:, xs])

@@ -1,5 +1,5 @@
 """Rehearsal of the N-rank render + gather on whatever GPUs the box has (ranks may share one):
-each rank renders its tile (tiles.DEAL: 8-column bands; YK_DEAL=rows: single rows) into device memory through the C-ABI, the tiles go to
+each rank renders its tile (tiles.DEAL: single rows; YK_DEAL=cols: 8-column bands) into device memory through the C-ABI, the tiles go to
 rank 0 through uecraytracing_amd.tiles.TileGather, and rank 0 compares the assembled image with
 a single-process render of the whole image.  Launch with torchrun; YK_BENCH_BACKEND=gloo when
 ranks share a GPU (RCCL needs one GPU per rank).

@@ -152,6 +152,10 @@ constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
 #endif
 constexpr uint32_t kClaimTail = YK_CLAIM_TAIL, kClaimTailFactor = YK_CLAIM_TAIL_FACTOR;
 static_assert(kClaimTail == 0 || (kClaimTail >= 64 && kClaimTail <= YK_CLAIM), "a tail claim serves a whole wave");
+// the FP64 kernel's candidate list as 64-bit (bound, index) entries (A/B, round 6)
+#ifndef YK_CAND64
+#define YK_CAND64 0
+#endif
 #ifndef YK_WG_HOLD
 #define YK_WG_HOLD 0
 #endif
@@ -1116,11 +1120,20 @@ void yk_render_persistent(KernelArgs ka) {
         const float tmin_lo = __double2float_rd(ka.t_min) * (1.0f - 0x1p-17f);
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
         float ustar_f = INFINITY;  // >= ustar * (1 + 2^-18)
-        uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        uint32_t nc = 0;
         // candidate lower bounds kept as floats RN(L), compared with ustar_f >= RN(U*): by
         // monotone rounding (all bounds >= 0) L <= U* implies RN(L) <= ustar_f, so the float
         // comparison only ever keeps MORE candidates than the double comparison would
+#if YK_CAND64
+        // each entry one 64-bit register pair (RN(L) bits << 32 | tuple index): a shift of the list
+        // is three v_mov_b64
+        uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+#define YK_QL(q) __uint_as_float((uint32_t)((q) >> 32))
+#define YK_QI(q) ((uint32_t)(q))
+#else
+        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
+#endif
         // overflow of the stack or of the candidate list is recorded as nc = 5, not as a flag of
         // its own: a bool carried round the traversal loop lives in a lane mask that every
         // divergent exit has to merge (-3.4% as a bool), an integer flag is one more loop-carried
@@ -1235,6 +1248,24 @@ void yk_render_persistent(KernelArgs ka) {
                 ustar = ub;
                 ustar_f = (float)ub * (1.0f + 0x1p-18f);
               }
+#if YK_CAND64
+              if (nc == 4) {  // compact: drop entries the new bound has excluded
+                uint32_t m2 = 0;
+                const uint64_t d0 = q0, d1 = q1, d2 = q2, d3 = q3;
+#define YK_QSET(K, V) do { if ((K) == 0) q0 = V; else if ((K) == 1) q1 = V; else if ((K) == 2) q2 = V; else q3 = V; } while (0)
+                if (YK_QL(d0) <= ustar_f) { YK_QSET(m2, d0); ++m2; }
+                if (YK_QL(d1) <= ustar_f) { YK_QSET(m2, d1); ++m2; }
+                if (YK_QL(d2) <= ustar_f) { YK_QSET(m2, d2); ++m2; }
+                if (YK_QL(d3) <= ustar_f) { YK_QSET(m2, d3); ++m2; }
+#undef YK_QSET
+                nc = m2;
+              }
+              if (nc < 4) {
+                q3 = q2, q2 = q1, q1 = q0;
+                q0 = ((uint64_t)__float_as_uint((float)lb) << 32) | id;
+                ++nc;
+              } else {
+#else
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
                 uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
@@ -1255,6 +1286,7 @@ void yk_render_persistent(KernelArgs ka) {
                 c0 = id, l0 = (float)lb;
                 ++nc;
               } else {
+#endif
                 nc = 5;  // the list is full: overflow (the exact linear scan decides)
               }
             } while (0);
@@ -1272,10 +1304,17 @@ void yk_render_persistent(KernelArgs ka) {
           // candidate of a ray, so its refined reciprocal is computed once
           const bool a_ok = ykd::div_range(a);
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
+#if YK_CAND64
+          if (nc > 0 && YK_QL(q0) <= ustar_f) exact_candidate(geo, YK_QI(q0), o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 1 && YK_QL(q1) <= ustar_f) exact_candidate(geo, YK_QI(q1), o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 2 && YK_QL(q2) <= ustar_f) exact_candidate(geo, YK_QI(q2), o, d, a, ra, a_ok, ka.t_min, hit);
+          if (nc > 3 && YK_QL(q3) <= ustar_f) exact_candidate(geo, YK_QI(q3), o, d, a, ra, a_ok, ka.t_min, hit);
+#else
           if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 1 && l1 <= ustar_f) exact_candidate(geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 2 && l2 <= ustar_f) exact_candidate(geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 3 && l3 <= ustar_f) exact_candidate(geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
+#endif
         }
       }
       if (linear) {
@@ -2177,6 +2216,12 @@ struct ykgpu_context {
   std::vector<hipEvent_t> lev_prev;
   uint32_t lev_prev_used = 0;  // (events of the previous call in lev_prev: YKGPU_TIMELINE prints them)
   uint32_t prev_n = 0;
+  // per global launch number g (mod kDepRing): its render's end and its reduce's end, the events a
+  // later launch that reuses its start-record or colour buffer waits for, whichever call it was in
+  std::vector<hipEvent_t> gev;
+  // launches enqueued back to back with the current ring geometry (prev_geom), over calls: a call
+  // overlaps the ones before it only when the last max(ring depths) launches had its geometry
+  uint64_t run_len = 0;
   // the previous call's ring and scratch geometry: a call overlaps it only when every field is
   // equal (launch() `ov`; equal slot offsets in every ring buffer and scratch slice)
   struct RingGeom {
@@ -2348,14 +2393,19 @@ constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
 #define YK_LAUNCHES_PER_CALL 32
 #endif
 constexpr uint32_t kLaunchesPerCall = YK_LAUNCHES_PER_CALL;
-// ... and at least kLaunchSlots sample slots per launch when the tile is small: a launch has a
-// fixed cost (its warm-up, the ramp of its persistent grid, a reduce), so a thin row tile needs
-// more samples per launch (8-way tile of 1920x1080x512, 135 rows: 31.5 ms at 32 spp per launch,
-// 28.8 at 64, 28.2 at 128, 29.4 at 256 — the full frame's best launch, 32 spp, is 66M slots)
+// ... and launches of about kLaunchSlots sample slots when the tile is small: a launch has a fixed
+// cost (the handover of every CU from its render workgroup to the next launch's, filled by seed
+// walks: ~0.2 ms per launch), so a call is split into round(slots / kLaunchSlots)
+// launches — the frame's 32-spp launches are 66M slots, and a tile's launches are as large (the
+// 8-way tile of 1920x1080x512: 2 launches of 256 spp; with 2^25-slot launches, 4 of 128, its
+// back-to-back calls cost 2% more per sample than the frame's, profiles/r06_ab/tiles/)
 #ifndef YK_LAUNCH_SLOTS
-#define YK_LAUNCH_SLOTS (1u << 25)
+#define YK_LAUNCH_SLOTS (1u << 26)
 #endif
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
+// global launch numbers whose dependency events (ykgpu_context::gev) are kept: more than any ring
+// is deep
+constexpr uint32_t kDepRing = 16;
 // Under memory pressure (launch()): launches shrink down to this many sample slots before a call
 // fails with YK_ERR_NOMEM, and the rings leave kMemReserve of the device free
 constexpr uint64_t kMemFloorSlots = 1ull << 24;
@@ -2552,7 +2602,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
   uint64_t launch_slots = kLaunchSlots;  // (A/B knob: YKGPU_LAUNCH_SLOTS)
   if (const char* e = ab_knob("YKGPU_LAUNCH_SLOTS")) launch_slots = (uint64_t)std::max(1ll, std::atoll(e));
-  const uint64_t slot_spp = (launch_slots + nps - 1) / nps;
+  const uint64_t call_launches = std::max<uint64_t>(1, ((uint64_t)nps * spp + launch_slots / 2) / launch_slots);
+  const uint64_t slot_spp = (spp + call_launches - 1) / call_launches;
   // A long call takes longer launches: every launch pays a drain whose length is the longest path
   // of its last samples, and many launches per call buy nothing once there are ~32 (config 5,
   // 1920x1080x4096 at depth 200 on the glass scene: 32 spp per launch 1730 ms, 64 1631, 121 (the
@@ -2619,28 +2670,41 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     if (const char* e = ab_knob(inflight ? "YKGPU_SCHED_GROW_OV" : "YKGPU_SCHED_GROW"))
       grow_k = (uint32_t)std::max(2, std::atoi(e));
     sched.clear();
-    for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
-      uint32_t take = std::min(k, spp - s0);
-      const uint32_t rest = spp - (s0 + take);
-      if (rest > 0 && rest < std::max(1u, take / 4)) {
-        // a short tail launch would cost its own ramp and drain: fold it in, or split the
-        // remainder into two equal launches when one would exceed the colour budget
-        take = spp - s0 <= kmax ? spp - s0 : (spp - s0 + 1) / 2;
-      }
+    // the ramp (launches below kmax), then the rest in the fewest launches of at most kmax, spread
+    // evenly: no launch exceeds kmax, so every call of the same kmax places its launches in the
+    // rings alike and a back-to-back call overlaps the call before it, synced or not (a rest short
+    // of a quarter of the ramp's last launch joins that launch instead of paying its own drain)
+    uint32_t s0 = 0;
+    for (uint32_t k = std::min(first_k, kmax); k < kmax && s0 < spp; k = std::min(grow_k * k, kmax)) {
+      const uint32_t take = std::min(k, spp - s0);
       sched.emplace_back(s0, take);
       s0 += take;
-      k = std::min(grow_k * k, kmax);
     }
-    K = 0;  // largest launch
-    for (auto& l : sched) K = std::max(K, l.second);
+    if (s0 < spp && !sched.empty() && spp - s0 < sched.back().second / 4 && sched.back().second + (spp - s0) <= kmax) {
+      sched.back().second += spp - s0;  // a short rest joins the ramp's last launch
+      s0 = spp;
+    }
+    if (s0 < spp) {
+      const uint32_t rest = spp - s0, n = (rest + kmax - 1) / kmax;
+      for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t take = rest / n + (q < rest % n ? 1u : 0u);
+        sched.emplace_back(s0, take);
+        s0 += take;
+      }
+    }
+    // a launch buffer of the rings holds kmax samples per pixel (every launch fits: above)
+    K = kmax;
     nlaunch = (uint32_t)sched.size();
-    kWarmRing = std::min(nlaunch, kWarmRingDepth);
+    // rings as deep as kWarmRingDepth / col_ring() whatever the call's launch count (a call of two
+    // launches reuses the buffers of the call before it, launch() `ov`); one buffer each for a
+    // single-launch call
+    kWarmRing = nlaunch > 1 ? kWarmRingDepth : 1;
     if (const char* e = ab_knob("YKGPU_WARM_RING"))  // (A/B) launch buffers in the ring
-      kWarmRing = (uint32_t)std::min<uint64_t>(nlaunch, (uint64_t)std::max(2, std::atoi(e)));
+      kWarmRing = (uint32_t)std::min<uint64_t>(kDepRing - 1, (uint64_t)std::max(2, std::atoi(e)));
     if (warm_first) kWarmRing = nlaunch;
     // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
     // reduce c (stream red) overlaps the renders after it
-    kColRing = std::min(nlaunch, col_ring());
+    kColRing = nlaunch > 1 ? std::min(col_ring(), kDepRing - 1) : 1;
     const size_t need_warm = x128 ? 0 : (size_t)kWarmRing * nps * K * welem;
     const size_t need_col = (size_t)kColRing * nps * K * kColStride * sizeof(double);
     if (kmax > kfloor && (need_warm > ctx->warm_cap || need_col > ctx->col_cap * sizeof(double))) {
@@ -2835,8 +2899,11 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   geom.mt = ctx->d_mt;
   geom.ids = ctx->d_ids;
   const char* ove = std::getenv("YKGPU_OVERLAP");
+  // (the last max(ring) launches, of however many calls, had this geometry: each buffer this call
+  // reuses was last used by one of them, whose events ctx->gev holds)
+  const bool same_run = ctx->prev_ok && ctx->prev_geom == geom;  // (ctx->run_len continues)
   const bool ov = !x128 && !warm_first && !(ove && std::atoi(ove) == 0) && ctx->prev_ok && ctx->prev_geom == geom &&
-                  ctx->prev_n >= std::max(kWarmRing, kColRing);
+                  ctx->run_len >= std::max(kWarmRing, kColRing) && std::max(kWarmRing, kColRing) < kDepRing;
   if (ctx->dirty && (rc = quiesce(ctx))) return rc;  // a failed call's work: wait it out on the host
   const bool after_prev = ctx->prev_enqueued && !ctx->dirty && !ov;
   ctx->prev_ok = false;  // (until this call has been enqueued)
@@ -2888,14 +2955,20 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
       if (after_prev) YK_HIP(hipStreamWaitEvent(s, ctx->lev_prev[6 * (ctx->prev_n - 1) + 5], 0));
     }
   }
-  const uint32_t pn = ctx->prev_n;
+  while (ctx->gev.size() < 2ull * kDepRing) {
+    hipEvent_t e;
+    YK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->gev.push_back(e);
+  }
+  // the end of global launch g's render ([0]) or reduce ([1])
+  auto gdep = [&](uint64_t g, int which) { return ctx->gev[2 * (g % kDepRing) + which]; };
   auto warm = [&](uint32_t c) -> int {
     hipEvent_t* ev = &ctx->lev[6 * c];
-    // its buffer: the render that last read it (launch c - ring, possibly the previous call's)
+    // its buffer: the render that last read it (launch c - ring, possibly an earlier call's)
     if (c >= kWarmRing)
       YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev[6 * (c - kWarmRing) + 3], 0));
     else if (ov)
-      YK_HIP(hipStreamWaitEvent(ctx->aux, ctx->lev_prev[6 * (pn - kWarmRing + c) + 3], 0));
+      YK_HIP(hipStreamWaitEvent(ctx->aux, gdep(g0 + c - kWarmRing, 0), 0));
     wa.s0 = sched[c].first;
     wa.n = (uint64_t)nps * sched[c].second;
     wa.out = ctx->d_warm + (size_t)((g0 + c) % kWarmRing) * nps * K * welem;
@@ -2946,7 +3019,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     if (c >= kColRing)
       YK_HIP(hipStreamWaitEvent(rs, ctx->lev[6 * (c - kColRing) + 5], 0));
     else if (ov)
-      YK_HIP(hipStreamWaitEvent(rs, ctx->lev_prev[6 * (pn - kColRing + c) + 5], 0));
+      YK_HIP(hipStreamWaitEvent(rs, gdep(g0 + c - kColRing, 1), 0));
     ka.pixel_counter = ctx->d_counter + (x128 ? c : (uint32_t)(g % kWarmRing));
     ka.clk = ctx->d_clk + 4 * c;
 #ifdef YK_DRAIN_DIAG
@@ -2964,6 +3037,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
                          dim3(grid), dim3(block), plan.lds_bytes, rs, ka);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[3], rs));
+    YK_HIP(hipEventRecord(gdep(g, 0), rs));
     ra.col = col;
     ra.nsl = nsl;
     ra.ks = ks;
@@ -2975,6 +3049,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     hipLaunchKernelGGL(yk_reduce_samples, dim3(reduce_blocks(ctx, nps)), dim3(256), 0, ctx->red, ra);
     YK_HIP(hipGetLastError());
     YK_HIP(hipEventRecord(ev[5], ctx->red));
+    YK_HIP(hipEventRecord(gdep(g, 1), ctx->red));
     if (c + kWarmRing < nlaunch && (rc = warm(c + kWarmRing))) return rc;
     ++launches;
   }
@@ -2982,6 +3057,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   YK_HIP(hipEventRecord(ctx->ev1, st));
   ctx->g_next = g0 + nlaunch;
   ctx->prev_n = nlaunch;
+  ctx->run_len = (same_run ? ctx->run_len : 0) + nlaunch;
   ctx->prev_geom = geom;
   ctx->prev_shape = shape;
   ctx->prev_ok = !x128 && !warm_first;
@@ -3284,6 +3360,7 @@ int ykgpu_context_destroy(ykgpu_context* ctx) {
   (void)hipFree(ctx->d_sums);
   for (hipEvent_t e : ctx->lev) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->lev_prev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->gev) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -13,19 +13,21 @@ moves equal-sized buffers), the tiles are gathered to rank 0 with one collective
 with backend 'nccl'; 'gloo' on CPU tensors in the tests), and rank 0 de-interleaves them with one
 index_select.
 
-Column dealing (round 4, the default of the N-rank bench: DEAL = "cols"): every rank renders
-every row, and the columns are dealt in bands of 2^COL_BAND_LOG2 = 8, band b → rank b mod N.
-A rank's 8x8 processing blocks are then 8x8 blocks of the IMAGE, as in the single-GPU frame,
-where a row-dealt tile's blocks span 8 x 16 to 32 x 16 image pixels (every N-th row) and their
-rays diverge more.  Columns vary in cost far less than rows (the sky is at the
-top), so cyclic 8-column bands balance the ranks as well.  The tile is uint8[H, cols_max, 3];
-rank 0 de-interleaves the gathered tiles with one index_select over pixels.
+Single rows are the N-rank bench's default (DEAL = "rows", round 6: north_star's "row-tiled"),
+and the drop-in's device group deals them too (ykgpu_group_render), so one partition ships.
+Column dealing (rounds 4-5's default, `bench.py --deal cols`): every rank renders every row, and
+the columns are dealt in bands of 2^COL_BAND_LOG2 = 8, band b → rank b mod N, so a rank's 8x8
+processing blocks are 8x8 blocks of the image, where a row-dealt tile's blocks span every N-th
+row.  Measured like the contract loop (profiles/r06_ab/tiles/r06e_deal8.txt), the
+two are equal at 8 ranks within 0.4% (slowest tile 1.048-1.053 x frame/8 either way at K = 8);
+8-row bands balance worse (1.083).  A column tile is uint8[H, cols_max, 3]; rank 0
+de-interleaves the gathered tiles with one index_select over pixels.
 """
 from __future__ import annotations
 
 BAND_LOG2 = 0
 COL_BAND_LOG2 = 3
-DEAL = "cols"
+DEAL = "rows"
 
 
 def tile_rows(rank: int, world: int, height: int, band_log2: int = BAND_LOG2):
