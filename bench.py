@@ -372,8 +372,10 @@ def rank_tiles(ren, stream, seed0, frame, deal, steps, warmup):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)  # single steps vary by up to ±3% (profiles/r03_ab/variance/): 8 steps ≈ 1.5 s
-    ap.add_argument("--warmup", type=int, default=2)
+    # the driver's own run: --steps 20 --warmup 5 (BENCH_r05.json); the per-rank tiles are timed over
+    # the same number of calls (rank_tiles)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--depth", type=int, default=50)

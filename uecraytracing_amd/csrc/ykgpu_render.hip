@@ -152,10 +152,6 @@ constexpr uint32_t kClaim = YK_CLAIM;  // sample slots a wave claims per atomic
 #endif
 constexpr uint32_t kClaimTail = YK_CLAIM_TAIL, kClaimTailFactor = YK_CLAIM_TAIL_FACTOR;
 static_assert(kClaimTail == 0 || (kClaimTail >= 64 && kClaimTail <= YK_CLAIM), "a tail claim serves a whole wave");
-// the FP64 kernel's candidate list as 64-bit (bound, index) entries (A/B, round 6)
-#ifndef YK_CAND64
-#define YK_CAND64 0
-#endif
 #ifndef YK_WG_HOLD
 #define YK_WG_HOLD 0
 #endif
@@ -1124,16 +1120,8 @@ void yk_render_persistent(KernelArgs ka) {
         // candidate lower bounds kept as floats RN(L), compared with ustar_f >= RN(U*): by
         // monotone rounding (all bounds >= 0) L <= U* implies RN(L) <= ustar_f, so the float
         // comparison only ever keeps MORE candidates than the double comparison would
-#if YK_CAND64
-        // each entry one 64-bit register pair (RN(L) bits << 32 | tuple index): a shift of the list
-        // is three v_mov_b64
-        uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-#define YK_QL(q) __uint_as_float((uint32_t)((q) >> 32))
-#define YK_QI(q) ((uint32_t)(q))
-#else
         uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
-#endif
         // overflow of the stack or of the candidate list is recorded as nc = 5, not as a flag of
         // its own: a bool carried round the traversal loop lives in a lane mask that every
         // divergent exit has to merge (-3.4% as a bool), an integer flag is one more loop-carried
@@ -1248,24 +1236,6 @@ void yk_render_persistent(KernelArgs ka) {
                 ustar = ub;
                 ustar_f = (float)ub * (1.0f + 0x1p-18f);
               }
-#if YK_CAND64
-              if (nc == 4) {  // compact: drop entries the new bound has excluded
-                uint32_t m2 = 0;
-                const uint64_t d0 = q0, d1 = q1, d2 = q2, d3 = q3;
-#define YK_QSET(K, V) do { if ((K) == 0) q0 = V; else if ((K) == 1) q1 = V; else if ((K) == 2) q2 = V; else q3 = V; } while (0)
-                if (YK_QL(d0) <= ustar_f) { YK_QSET(m2, d0); ++m2; }
-                if (YK_QL(d1) <= ustar_f) { YK_QSET(m2, d1); ++m2; }
-                if (YK_QL(d2) <= ustar_f) { YK_QSET(m2, d2); ++m2; }
-                if (YK_QL(d3) <= ustar_f) { YK_QSET(m2, d3); ++m2; }
-#undef YK_QSET
-                nc = m2;
-              }
-              if (nc < 4) {
-                q3 = q2, q2 = q1, q1 = q0;
-                q0 = ((uint64_t)__float_as_uint((float)lb) << 32) | id;
-                ++nc;
-              } else {
-#else
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
                 uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
@@ -1286,7 +1256,6 @@ void yk_render_persistent(KernelArgs ka) {
                 c0 = id, l0 = (float)lb;
                 ++nc;
               } else {
-#endif
                 nc = 5;  // the list is full: overflow (the exact linear scan decides)
               }
             } while (0);
@@ -1304,17 +1273,10 @@ void yk_render_persistent(KernelArgs ka) {
           // candidate of a ray, so its refined reciprocal is computed once
           const bool a_ok = ykd::div_range(a);
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
-#if YK_CAND64
-          if (nc > 0 && YK_QL(q0) <= ustar_f) exact_candidate(geo, YK_QI(q0), o, d, a, ra, a_ok, ka.t_min, hit);
-          if (nc > 1 && YK_QL(q1) <= ustar_f) exact_candidate(geo, YK_QI(q1), o, d, a, ra, a_ok, ka.t_min, hit);
-          if (nc > 2 && YK_QL(q2) <= ustar_f) exact_candidate(geo, YK_QI(q2), o, d, a, ra, a_ok, ka.t_min, hit);
-          if (nc > 3 && YK_QL(q3) <= ustar_f) exact_candidate(geo, YK_QI(q3), o, d, a, ra, a_ok, ka.t_min, hit);
-#else
           if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 1 && l1 <= ustar_f) exact_candidate(geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 2 && l2 <= ustar_f) exact_candidate(geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 3 && l3 <= ustar_f) exact_candidate(geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
-#endif
         }
       }
       if (linear) {
