@@ -2632,27 +2632,22 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     if (const char* e = ab_knob(inflight ? "YKGPU_SCHED_GROW_OV" : "YKGPU_SCHED_GROW"))
       grow_k = (uint32_t)std::max(2, std::atoi(e));
     sched.clear();
-    // the ramp (launches below kmax), then the rest in the fewest launches of at most kmax, spread
-    // evenly: no launch exceeds kmax, so every call of the same kmax places its launches in the
-    // rings alike and a back-to-back call overlaps the call before it, synced or not (a rest short
-    // of a quarter of the ramp's last launch joins that launch instead of paying its own drain)
-    uint32_t s0 = 0;
-    for (uint32_t k = std::min(first_k, kmax); k < kmax && s0 < spp; k = std::min(grow_k * k, kmax)) {
-      const uint32_t take = std::min(k, spp - s0);
+    // the ramp (first_k, growing by grow_k), then launches of kmax; a short tail launch, which would
+    // pay its own drain, is folded into the launch before it, or that launch and the tail are split
+    // into two equal launches when one would exceed kmax — so no launch exceeds kmax, and every call
+    // of the same kmax places its launches in the rings alike (a back-to-back call overlaps the
+    // call before it, synced or not).  Launches of exactly kmax also keep the warm-up's walks
+    // aligned: at 32 spp its grid-stride is the pixel count, so a lane's four walks are four
+    // samples of one pixel (their processing-order reads coincide; a 30- or 31-spp launch fetches
+    // 1.7x the bytes per slot in the warm-up, profiles/r06_ab/pmc/)
+    for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
+      uint32_t take = std::min(k, spp - s0);
+      const uint32_t rest = spp - (s0 + take);
+      if (rest > 0 && rest < std::max(1u, take / 4))
+        take = spp - s0 <= kmax ? spp - s0 : (spp - s0 + 1) / 2;
       sched.emplace_back(s0, take);
       s0 += take;
-    }
-    if (s0 < spp && !sched.empty() && spp - s0 < sched.back().second / 4 && sched.back().second + (spp - s0) <= kmax) {
-      sched.back().second += spp - s0;  // a short rest joins the ramp's last launch
-      s0 = spp;
-    }
-    if (s0 < spp) {
-      const uint32_t rest = spp - s0, n = (rest + kmax - 1) / kmax;
-      for (uint32_t q = 0; q < n; ++q) {
-        const uint32_t take = rest / n + (q < rest % n ? 1u : 0u);
-        sched.emplace_back(s0, take);
-        s0 += take;
-      }
+      k = std::min(grow_k * k, kmax);
     }
     // a launch buffer of the rings holds kmax samples per pixel (every launch fits: above)
     K = kmax;
