@@ -180,3 +180,41 @@ def test_two_and_three_launch_calls_back_to_back():
     xs = [x for x in range(1920) if (x >> 3) % 8 == 3]
     cpu, _, _, _ = oracle_lib.render(arr, cam, make_params(1920, 1080, 512, 50, 404, rows=(5, 2, 1070)), nthreads=16)
     np.testing.assert_array_equal(want[512][[5, 1075]], cpu[:, xs])
+
+
+def test_random_back_to_back_sequence_of_mixed_calls():
+    """A seeded random sequence of calls enqueued back to back without synchronisation — whole
+    frames and row / column tiles of 1920x1080 whose in-flight launches are 1, 2 or 3 per call
+    (launches of ~2^26 slots), small single-launch calls, FP32 and xor128 calls between them — so
+    calls of equal ring geometry overlap across calls of other geometries, of other launch counts
+    and of other modes (launch(): ctx->gev, run_len).  Every output equals the synced render of its
+    params."""
+    torch = pytest.importorskip("torch")
+    import random
+
+    from uecraytracing_amd.tiles import rank_tile
+    arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
+    shapes = [
+        make_params(1920, 1080, 64, 50, 404),                                   # 2 launches of 32
+        make_params(1920, 1080, 96, 50, 404),                                   # 3 launches of 32
+        make_params(1920, 1080, 512, 50, 404, **rank_tile(2, 8, 1080, 1920, "rows")),   # 2 of 256
+        make_params(1920, 1080, 768, 50, 404, **rank_tile(2, 8, 1080, 1920, "rows")),   # 3 of 256
+        make_params(1920, 1080, 256, 50, 404, **rank_tile(1, 4, 1080, 1920, "cols")),   # 2 of 128
+        make_params(320, 180, 16, 50, 404),                                     # 1 launch
+        make_params(320, 180, 16, 50, 404, precision=PRECISION_FP32),
+        make_params(320, 180, 16, 50, 404, rng=RNG_XOR128),
+    ]
+    rnd = random.Random(6)
+    seq = [rnd.randrange(len(shapes)) for _ in range(18)]
+    with yk.Renderer(0) as r:
+        r.set_scene(arr, cam)
+        want = {k: r.render(shapes[k]) for k in sorted(set(seq))}
+        outs = [torch.zeros((shapes[k].row_count, shapes[k].tile_width(), 3), dtype=torch.uint8, device="cuda:0")
+                for k in seq]
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        for k, o in zip(seq, outs):
+            r.render_async(shapes[k], o.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        for k, o in zip(seq, outs):
+            np.testing.assert_array_equal(o.cpu().numpy(), want[k])
