@@ -119,6 +119,15 @@ struct Wide {
   int n;
 };
 
+// the slot chosen for expansion (round 6 exploration): 0 the largest area (the library's rule),
+// 1 the largest area x leaves below, 2 the largest area x (leaves below)^0.5
+static int g_collapse = 0;
+static std::vector<uint32_t> g_leaves;  // leaves under each binary node
+static uint32_t count_leaves(const ykbvh::Built& b, int32_t code) {
+  if (code < 0) return 1;
+  if (g_leaves[code]) return g_leaves[code];
+  return g_leaves[code] = count_leaves(b, b.nodes[code].child[0]) + count_leaves(b, b.nodes[code].child[1]);
+}
 static void collapse(const ykbvh::Built& b, std::vector<Wide>& out, int32_t code, int width) {
   // code >= 0: binary node index
   struct E { float lo[3], hi[3]; int32_t code; };
@@ -130,10 +139,14 @@ static void collapse(const ykbvh::Built& b, std::vector<Wide>& out, int32_t code
     float dx = e.hi[0] - e.lo[0], dy = e.hi[1] - e.lo[1], dz = e.hi[2] - e.lo[2];
     return dx * dy + dy * dz + dz * dx;
   };
+  auto score = [&](const E& e) {
+    const double a = area(e), nl = e.code >= 0 ? count_leaves(b, e.code) : 1;
+    return g_collapse == 1 ? a * nl : g_collapse == 2 ? a * std::sqrt(nl) : a;
+  };
   while ((int)ents.size() < width) {
     int best = -1;
     for (size_t i = 0; i < ents.size(); ++i)
-      if (ents[i].code >= 0 && (best < 0 || area(ents[i]) > area(ents[best]))) best = (int)i;
+      if (ents[i].code >= 0 && (best < 0 || score(ents[i]) > score(ents[best]))) best = (int)i;
     if (best < 0) break;
     const ykbvh::Node& c = b.nodes[ents[best].code];
     E e0{{c.lo_x[0], c.lo_y[0], c.lo_z[0]}, {c.hi_x[0], c.hi_y[0], c.hi_z[0]}, c.child[0]};
@@ -181,6 +194,8 @@ int main(int argc, char** argv) {
   ykbvh::Options opt;
   if (argc > 3) opt.max_leaf = atoi(argv[3]);
   if (argc > 4) opt.bins = atoi(argv[4]);
+  opt.all_axes = argc > 5 ? atoi(argv[5]) != 0 : true;  // (the FP64 tree: all three axes)
+  if (argc > 6) g_collapse = atoi(argv[6]);
   Sim sim;
   uint32_t n = 0;
   yk_camera cam;
@@ -272,6 +287,7 @@ int main(int argc, char** argv) {
          sum_max / sum_mean);
   // ---- lockstep wave model: binary vs 4-wide, while-while loop as compiled
   std::vector<Wide> wide;
+  g_leaves.assign(sim.bvh.nodes.size(), 0);
   if (sim.bvh.root >= 0) collapse(sim.bvh, wide, sim.bvh.root, 4);
   std::vector<size_t> idx(seg.size());
   for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
