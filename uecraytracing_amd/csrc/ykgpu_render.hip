@@ -1116,11 +1116,10 @@ void yk_render_persistent(KernelArgs ka) {
         const float tmin_lo = __double2float_rd(ka.t_min) * (1.0f - 0x1p-17f);
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
         float ustar_f = INFINITY;  // >= ustar * (1 + 2^-18)
-        uint32_t nc = 0;
+        uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
         // candidate lower bounds kept as floats RN(L), compared with ustar_f >= RN(U*): by
         // monotone rounding (all bounds >= 0) L <= U* implies RN(L) <= ustar_f, so the float
         // comparison only ever keeps MORE candidates than the double comparison would
-        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
         float l0 = 0, l1 = 0, l2 = 0, l3 = 0;
         // overflow of the stack or of the candidate list is recorded as nc = 5, not as a flag of
         // its own: a bool carried round the traversal loop lives in a lane mask that every
