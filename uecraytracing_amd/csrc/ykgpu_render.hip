@@ -134,6 +134,11 @@ constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp buil
 // would be skipped silently).
 constexpr uint32_t kLeafCapF64 = 1, kLeafCapF32 = 2;
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
+// FP64 node visit without a branch: the stack's bottom entry holds the empty leaf (a sentinel), so
+// "no slot entered" pops unconditionally and every lane of the visit runs the same instructions
+#ifndef YK_NODE_BF
+#define YK_NODE_BF 0
+#endif
 
 #ifndef YK_CLAIM
 #define YK_CLAIM 512
@@ -934,6 +939,9 @@ void yk_render_persistent(KernelArgs ka) {
   // barrier, so every wave-instruction below is one lane's (the profiler's per-wave FP64 counters
   // then count that lane's executed operations exactly: DESIGN.md §5)
   if (kCount && (ka.flags & kFlagOneLane) && lane != 0) return;
+#if YK_NODE_BF
+  stk[0] = ykbvh::kEmptyLeaf;  // the sentinel below every traversal's entries
+#endif
 #if YK_RENDER_PRIO
   // the warm-up waves sharing the SIMDs (priority 0) get only the issue slots the render leaves
   __builtin_amdgcn_s_setprio(YK_RENDER_PRIO);
@@ -1126,12 +1134,31 @@ void yk_render_persistent(KernelArgs ka) {
         // divergent exit has to merge (-3.4% as a bool), an integer flag is one more loop-carried
         // register (nc = 5 instead: -0.8%)
         int32_t node = ka.bvh_root;
+#if YK_NODE_BF
+        // this lane's traversal stack top as an LDS byte address (entries kBlk words apart), above
+        // the sentinel
+        const uint32_t stk_b = (uint32_t)(uintptr_t)stk;
+        uint32_t top = stk_b + kBlk * 4u;
+        const uint32_t stk_cap = stk_b + ka.stack_cap * kBlk * 4u;
+#define YK_STK(a) (*(__attribute__((address_space(3))) int32_t*)(uintptr_t)(a))
+#else
         int32_t* top = stk;  // this lane's traversal stack top (entries kBlk words apart)
         const int32_t* const stk_cap = stk + ka.stack_cap * kBlk;
+#endif
         for (;;) {
           if (node >= 0) {
+#if YK_NODE_BF
+           // the lane's run of interior nodes as a loop of its own tested at the bottom: its exit
+           // value is the visit's own result, so the compiler keeps node / top / nc in place
+           do {
+#endif
             if (kCount) ++n_node;
             YK_STAMP_NODE_ITERATION(lane);
+#if YK_NODE_BF
+            // the entry below the top (the sentinel when the stack holds nothing), read with the
+            // planes: the pushes below write at and above the top, never here
+            const int32_t popped = YK_STK(top - kBlk * 4u);
+#endif
             // near / far distances of the 4 slots per axis, one packed FMA per pair of slots:
             // t = plane*(1/d) - o*(1/d), the binary node's arithmetic per slot
             const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
@@ -1169,6 +1196,24 @@ void yk_render_persistent(KernelArgs ka) {
             // keep the child-code read in this block, issued with the plane reads (the compiler
             // would otherwise sink it into the branch below and wait for it there)
             asm volatile("" ::"v"(ch.x), "v"(ch.y), "v"(ch.z), "v"(ch.w));
+#if YK_NODE_BF
+            {
+              // the last slot entered is visited next, the others entered are pushed in slot
+              // order; none entered: the popped entry is next and the top moves down one
+              const bool any = hk[0] || hk[1] || hk[2] || hk[3];
+              node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : (hk[0] ? ch.x : popped)));
+              YK_STK(top) = ch.x;
+              top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlk * 4u : 0u;
+              YK_STK(top) = ch.y;
+              top += (hk[1] && (hk[2] || hk[3])) ? kBlk * 4u : 0u;
+              YK_STK(top) = ch.z;
+              top += (hk[2] && hk[3]) ? kBlk * 4u : (any ? 0u : 0u - kBlk * 4u);
+              // stack full: the top stays at the capacity and nc = 5 sends the lane to the scan
+              nc = top > stk_cap ? 5u : nc;
+              top = top > stk_cap ? stk_cap : top;
+            }
+           } while (node >= 0);
+#else
             if (hk[0] || hk[1] || hk[2] || hk[3]) {
               // the last slot entered is visited next and the others entered are pushed, in slot
               // order: no distance sort (visit order only affects how fast U* shrinks, never the
@@ -1200,7 +1245,13 @@ void yk_render_persistent(KernelArgs ka) {
               node = *top;
             }
             continue;
+#endif
+#if YK_NODE_BF
+          }
+          {
+#else
           } else {
+#endif
             YK_STAMP(2);  // interior nodes since the last stamp
             const uint32_t v = ~(uint32_t)node, first = v >> 4, cnt = v & 15u;
             // the FP64 tree has one sphere per leaf (max_leaf = 1: the builder's median fallback
@@ -1260,9 +1311,16 @@ void yk_render_persistent(KernelArgs ka) {
             } while (0);
             YK_STAMP(6);  // this leaf
           }
+#if YK_NODE_BF
+          if (top <= stk_b + kBlk * 4u) break;  // only the sentinel left, or the sentinel just visited
+          top -= kBlk * 4u;
+          node = YK_STK(top);
+#undef YK_STK
+#else
           if (top == stk) break;
           top -= kBlk;
           node = *top;
+#endif
         }
         YK_STAMP(2);
         if (nc > 4) {
