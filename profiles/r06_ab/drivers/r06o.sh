@@ -1,0 +1,16 @@
+# r06o: on the branch-free visit (YK_NODE_BF, r06n: -2.1%): the stack top held as the entry below
+# it plus child codes read from LDS address 0 (YK_NODE_BF=2: two VALU fewer per visit), and the
+# candidates' skip past an exact root already found (YK_CAND_SKIP); parity suite per variant,
+# synced A/B at 512 spp, bench A/B
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+T=r06o
+mkdir -p gpurun_out/$T
+for V in bf2 bfskip bf2skip; do
+  YKGPU_LIB_OVERRIDE=$PWD/uecraytracing_amd/lib/abl/libykgpu_$V.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_modes.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/$T/parity_$V.log 2>&1 || { echo PARITY_FAILED $V; tail -30 gpurun_out/$T/parity_$V.log; exit 1; }
+  echo $V; tail -1 gpurun_out/$T/parity_$V.log
+done
+timeout -k 10 900 python tools/abtime.py 512 base nodebf bf2 bfskip bf2skip > gpurun_out/$T/ab512.txt 2>&1 || { tail -20 gpurun_out/$T/ab512.txt; exit 2; }
+cat gpurun_out/$T/ab512.txt
+bash tools/gpu_bench_ab.sh r06o_bench nodebf bf2 bfskip bf2skip || exit 3

@@ -148,6 +148,54 @@ def test_lens_retry_ring_fallbacks_are_bit_exact():
     np.testing.assert_array_equal(np.array(res["retry64"]["32"]["rows"], dtype=np.uint8), want)
 
 
+_STACK_CODE = r'''
+import hashlib, json, os, sys
+sys.path.insert(0, os.environ["YK_ROOT"])
+import torch
+import uecraytracing_amd as yk
+from uecraytracing_amd.records import PRECISION_FP32, make_params
+arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
+out = {}
+with yk.Renderer(0) as r:
+    r.set_scene(arr, cam)
+    for name, prec in (("fp64", 0), ("fp32", PRECISION_FP32)):
+        p = make_params(192, 108, 16, 50, 404, flags=1, precision=prec)  # counting instance
+        sums = r.render_sums(p)
+        st = r.stats()
+        out[name] = {"sha": hashlib.sha256(sums.tobytes()).hexdigest(), "linear_scans": st["linear_scans"],
+                     "segments": st["segments"]}
+print(json.dumps(out))
+'''
+
+
+def test_shallow_checked_stack_overflows_to_the_linear_scan():
+    """The FP64 branch-free visit skips its stack check where the plan gives the stack its proven
+    depth (3 x wide depth + 1 entries, KernelArgs::stack_check = 0: every headline launch).  The
+    checked path — a scene whose LDS copy leaves less room — is forced by a test build
+    (Makefile TESTVARIANTS, -DYK_STACK_CAP_FORCE=5: five checked entries for both trees): lanes
+    whose traversal overflows the stack take the exact linear scan, so the float64 per-pixel sums
+    equal the product library's bit for bit in FP64 and FP32, with linear scans counted only in
+    the shallow build."""
+    import json
+    import subprocess
+    import sys
+    root = yk.LIB_DIR
+    repo = os.path.dirname(os.path.dirname(root))
+    res = {}
+    for name, lib in (("product", os.path.join(root, "libykgpu.so")), ("stack5", os.path.join(root, "abl", "libykgpu_stack5.so"))):
+        assert os.path.exists(lib), f"{lib}: built by uecraytracing_amd/csrc/Makefile (all)"
+        env = dict(os.environ, YKGPU_LIB_OVERRIDE=lib, YK_ROOT=repo)
+        pr = subprocess.run([sys.executable, "-c", _STACK_CODE], env=env, capture_output=True, text=True,
+                            timeout=240)
+        assert pr.returncode == 0, pr.stderr[-2000:]
+        res[name] = json.loads([ln for ln in pr.stdout.splitlines() if ln.startswith("{")][-1])
+    for prec in ("fp64", "fp32"):
+        assert res["stack5"][prec]["sha"] == res["product"][prec]["sha"]
+        assert res["stack5"][prec]["segments"] == res["product"][prec]["segments"]
+        assert res["stack5"][prec]["linear_scans"] > res["product"][prec]["linear_scans"]
+    assert res["product"]["fp64"]["linear_scans"] == 0
+
+
 def test_two_and_three_launch_calls_back_to_back():
     """Calls of an 8-way column tile of 1920x1080 (259,200 pixels): 512 spp is two launches of 256
     spp and 768 spp three (launches of ~2^26 slots, DESIGN §3), with launch buffers of kmax = 256

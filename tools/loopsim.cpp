@@ -819,5 +819,79 @@ int main(int argc, char** argv) {
            "per lane: visits %.2f leaf tests %.2f | cost %.0f\n",
            name[variant], trips / nw, wv / nw, wl / nw, wd2 / nw, lv / (64.0 * nw), ll / (64.0 * nw), cost / nw);
   }
+  // ---- round 6: the branch-free visit's while-while loop (YK_NODE_BF: an inner visit loop until
+  // every lane holds a leaf, then one leaf block, then the pops) and its speculative form (a visit
+  // whose last entered child is a leaf parks it and goes on with the entry below the new top, known
+  // in registers; the leaf block tests the parked leaf, else the lane's current leaf)
+  for (int spec = 0; spec < 2; ++spec) {
+    double vb = 0, lb = 0, db = 0, outer = 0, lv = 0, ll = 0;
+    size_t nw = 0;
+    for (size_t g = 0; g + 64 <= idx.size(); g += 64, ++nw) {
+      std::vector<Lane> lanes(64);
+      for (int k = 0; k < 64; ++k) {
+        Lane& L = lanes[k];
+        L.o = seg[idx[g + k]].first;
+        L.d = seg[idx[g + k]].second;
+        L.a = dot(L.d, L.d);
+        L.ix = rcp((float)L.d.x), L.iy = rcp((float)L.d.y), L.iz = rcp((float)L.d.z);
+        L.node = M.root;
+      }
+      for (;;) {
+        outer += 1;
+        for (;;) {  // inner: visits
+          bool any = false;
+          for (auto& L : lanes) {
+            if (L.done || L.node < 0) continue;
+            any = true;
+            ++lv;
+            const size_t before = L.stk.size();
+            M.visit(L);
+            const bool entered = !(L.stk.size() + 1 == before || (before == 0 && L.node == kDone && false));
+            // a pop inside the visit shrinks the stack by one; anything else entered a slot
+            const bool popped = L.stk.size() + 1 == before && L.node != kDone;
+            if (spec && !popped && entered && L.node < 0 && L.node != kDone && L.pend == kNone) {
+              L.pend = L.node;
+              M.pop(L);
+            }
+          }
+          if (!any) break;
+          vb += 1;
+        }
+        bool anyl = false;
+        int maxd = 0;
+        for (auto& L : lanes) {
+          if (L.done) continue;
+          int32_t leaf = kNone;
+          if (L.pend != kNone) {
+            leaf = L.pend;
+            L.pend = kNone;
+          } else if (L.node < 0 && L.node != kDone) {
+            leaf = L.node;
+            M.pop(L);
+          }
+          if (leaf != kNone) {
+            anyl = true;
+            auto [cnt, dp] = M.leaf(L, leaf);
+            ll += cnt;
+            maxd = std::max(maxd, dp);
+          }
+          // a lane still holding a leaf parks it (spec) or keeps it for the next block
+          if (spec && L.node < 0 && L.node != kDone && L.pend == kNone) {
+            L.pend = L.node;
+            M.pop(L);
+          }
+          if (L.node == kDone && L.pend == kNone) L.done = true;
+        }
+        lb += anyl;
+        db += maxd;
+        bool all = true;
+        for (auto& L : lanes) all = all && L.done;
+        if (all) break;
+      }
+    }
+    printf("%-22s per wave-segment: outer %.1f, visit blocks %.1f, leaf blocks %.1f, disc tails %.1f | per lane: visits %.2f leaf tests %.2f | cost %.0f\n",
+           spec ? "BF speculative" : "BF while-while", outer / nw, vb / nw, lb / nw, db / nw, lv / (64.0 * nw), ll / (64.0 * nw),
+           (c_trip * outer + c_visit * vb + c_leaf * lb + c_disc * db) / nw);
+  }
   return 0;
 }

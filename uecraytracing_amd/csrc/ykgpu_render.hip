@@ -134,10 +134,20 @@ constexpr int kCounters = 32;  // [16..18]: timeline, [19..22]: diag (stamp buil
 // would be skipped silently).
 constexpr uint32_t kLeafCapF64 = 1, kLeafCapF32 = 2;
 constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 x u16)
-// FP64 node visit without a branch: the stack's bottom entry holds the empty leaf (a sentinel), so
-// "no slot entered" pops unconditionally and every lane of the visit runs the same instructions
+// FP64 node visit without a branch (round 6): the stack's bottom entry holds the empty leaf (a
+// sentinel), so "no slot entered" pops unconditionally and every lane of the visit runs the same
+// instructions; a lane's run of interior nodes is a loop of its own (while-while), the entry below
+// the top read with the planes.  2: the loop variable is the address of that entry (constant DS
+// offsets for it and the pushes).  0: the round-5 visit with its push / pop branches (A/B).
+// 512 spp, same box (profiles/r06_ab/nodebf/): 0 -> 1: bench 163.0 -> 159.5 ms; 2 = 1.
 #ifndef YK_NODE_BF
-#define YK_NODE_BF 0
+#define YK_NODE_BF 2
+#endif
+// the FP64 stack sized to the tree's proven depth (3 x wide depth + 1 entries) where LDS allows,
+// its overflow check then skipped (a scalar branch on KernelArgs::stack_check): bench 159.0 ->
+// 156.2 ms on top of YK_NODE_BF (0: always checked, A/B)
+#ifndef YK_STACK_EXACT
+#define YK_STACK_EXACT 1
 #endif
 
 #ifndef YK_CLAIM
@@ -185,7 +195,9 @@ struct KernelArgs {
   CamF camf;
   uint32_t W, H, spp, max_depth;
   uint32_t seed0, row_begin, row_count, row_stride, band_log2;
-  uint32_t nspheres, pad_n, flags, id_stride;
+  // stack_check: 0 when the FP64 traversal stack holds 3 x (wide depth) + 1 entries, so the
+  // branch-free visit cannot overflow it and skips the check (upload_tree)
+  uint32_t nspheres, stack_check, flags, id_stride;
   // A launch renders samples [s0, s0 + nsl / npix_slots) of every pixel: sample slot
   // i = s_local * npix_slots + p is sample s0 + s_local of tile pixel order[p].
   uint32_t s0, nsl, npix_slots, seed_mode;  // seed_mode: YK_SEED_*
@@ -929,6 +941,10 @@ void yk_render_persistent(KernelArgs ka) {
     }
     __syncthreads();
     nodes = smem;
+#if YK_NODE_BF
+    // the child-code reads address the LDS copy from 0: the dynamic region must start there
+    if ((uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem != 0u) __builtin_trap();
+#endif
     leaf_geo = (const SphereGeo*)(smem + ka.lds_geo_off);
     leaf_ids = (const uint32_t*)(smem + ka.lds_ids_off);
     geo = (const SphereGeo*)(smem + ka.lds_tgeo_off);
@@ -1137,9 +1153,12 @@ void yk_render_persistent(KernelArgs ka) {
 #if YK_NODE_BF
         // this lane's traversal stack top as an LDS byte address (entries kBlk words apart), above
         // the sentinel
+        // (YK_NODE_BF 2: the variable holds the address of the entry BELOW the top, kTopOff less,
+        // so the visit's read of that entry and the pushes at the top take constant DS offsets)
+        constexpr uint32_t kTopOff = YK_NODE_BF == 2 ? kBlk * 4u : 0u;
         const uint32_t stk_b = (uint32_t)(uintptr_t)stk;
-        uint32_t top = stk_b + kBlk * 4u;
-        const uint32_t stk_cap = stk_b + ka.stack_cap * kBlk * 4u;
+        uint32_t top = stk_b + kBlk * 4u - kTopOff;
+        const uint32_t stk_cap = stk_b + ka.stack_cap * kBlk * 4u - kTopOff;
 #define YK_STK(a) (*(__attribute__((address_space(3))) int32_t*)(uintptr_t)(a))
 #else
         int32_t* top = stk;  // this lane's traversal stack top (entries kBlk words apart)
@@ -1157,14 +1176,27 @@ void yk_render_persistent(KernelArgs ka) {
 #if YK_NODE_BF
             // the entry below the top (the sentinel when the stack holds nothing), read with the
             // planes: the pushes below write at and above the top, never here
-            const int32_t popped = YK_STK(top - kBlk * 4u);
+            const int32_t popped = YK_STK(top + kTopOff - kBlk * 4u);
 #endif
             // near / far distances of the 4 slots per axis, one packed FMA per pair of slots:
             // t = plane*(1/d) - o*(1/d), the binary node's arithmetic per slot
             const f4 qnx = *(const f4*)(px + node), qfx = *(const f4*)(px + node + 16);
             const f4 qny = *(const f4*)(py + node), qfy = *(const f4*)(py + node + 16);
             const f4 qnz = *(const f4*)(pz + node), qfz = *(const f4*)(pz + node + 16);
+#if YK_NODE_BF
+            // the scene's LDS copy starts at LDS address 0 (the kernel's only LDS is the dynamic
+            // region, checked at the kernel's start), so the child codes of node n sit at n + 144
+            int4 ch;
+            if (kSceneInLds) {
+              typedef int i4v __attribute__((ext_vector_type(4)));
+              const i4v c4 = *(__attribute__((address_space(3))) const i4v*)(uintptr_t)((uint32_t)node + 144u);
+              ch = make_int4(c4.x, c4.y, c4.z, c4.w);
+            } else {
+              ch = *(const int4*)(nodes + node + 144);
+            }
+#else
             const int4 ch = *(const int4*)(nodes + node + 144);
+#endif
             bool hk[4];
 #if YK_SLAB_PAIRS_F64
             const f2 nx[2] = {slab_fma(qnx.xy, sxp), slab_fma(qnx.zw, sxp)};
@@ -1202,15 +1234,22 @@ void yk_render_persistent(KernelArgs ka) {
               // order; none entered: the popped entry is next and the top moves down one
               const bool any = hk[0] || hk[1] || hk[2] || hk[3];
               node = hk[3] ? ch.w : (hk[2] ? ch.z : (hk[1] ? ch.y : (hk[0] ? ch.x : popped)));
-              YK_STK(top) = ch.x;
+              YK_STK(top + kTopOff) = ch.x;
               top += (hk[0] && (hk[1] || hk[2] || hk[3])) ? kBlk * 4u : 0u;
-              YK_STK(top) = ch.y;
+              YK_STK(top + kTopOff) = ch.y;
               top += (hk[1] && (hk[2] || hk[3])) ? kBlk * 4u : 0u;
-              YK_STK(top) = ch.z;
+              YK_STK(top + kTopOff) = ch.z;
               top += (hk[2] && hk[3]) ? kBlk * 4u : (any ? 0u : 0u - kBlk * 4u);
               // stack full: the top stays at the capacity and nc = 5 sends the lane to the scan
-              nc = top > stk_cap ? 5u : nc;
-              top = top > stk_cap ? stk_cap : top;
+              // (only where the plan could not give the stack its proven depth: ka.stack_check)
+              if (ka.stack_check) {
+                asm volatile("");  // (a scalar branch: no selects on the uniform flag)
+                // signed: with YK_NODE_BF 2 the pop of the sentinel leaves `top` one entry below the
+                // stack's base, below LDS address 0 for the low lanes of a scene with a small LDS
+                // copy (unsigned, that wrapped past the capacity and the lane never left the loop)
+                nc = (int32_t)top > (int32_t)stk_cap ? 5u : nc;
+                top = (int32_t)top > (int32_t)stk_cap ? stk_cap : top;
+              }
             }
            } while (node >= 0);
 #else
@@ -1312,9 +1351,9 @@ void yk_render_persistent(KernelArgs ka) {
             YK_STAMP(6);  // this leaf
           }
 #if YK_NODE_BF
-          if (top <= stk_b + kBlk * 4u) break;  // only the sentinel left, or the sentinel just visited
+          if (top + kTopOff <= stk_b + kBlk * 4u) break;  // only the sentinel left, or the sentinel just visited
           top -= kBlk * 4u;
-          node = YK_STK(top);
+          node = YK_STK(top + kTopOff);
 #undef YK_STK
 #else
           if (top == stk) break;
@@ -2193,6 +2232,7 @@ struct DevTree {
   struct Plan {
     bool in_lds = false;
     uint32_t lds_bytes = 0, stack_off = 0, stack_cap = 0, stack_entries = 0;
+    bool stack_check = true;  // the kernel checks the stack top against stack_cap
     uint32_t tgeo_off = 0, mat_off = 0;  // shading tables in LDS (FP64 kernel), 0: none
     int grid = 0;                        // persistent blocks: occupancy x CUs
   } plan[2];
@@ -2877,7 +2917,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.nps_sh = wa.nps_sh;
   ka.w_m = wa.w_m;
   ka.w_sh = wa.w_sh;
-  ka.pad_n = 0;
+  ka.stack_check = plan.stack_check ? 1u : 0u;
   ReduceArgs ra;
   ra.acc = ctx->d_acc;
   ra.order = ctx->d_order;
@@ -3203,7 +3243,7 @@ int finish_stats(ykgpu_context* ctx) {
 // (for the occupancy).
 int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& centers, const std::vector<double>& radii,
                 double cam_ext, const ykbvh::Options& opt, uint32_t leaf_cap, const void* geo, size_t elem,
-                size_t tgeo_elem, const RenderKernel (&kern)[2][2]) {
+                size_t tgeo_elem, const RenderKernel (&kern)[2][2], bool exact_stack) {
   const uint32_t count = (uint32_t)radii.size();
   if (opt.max_leaf > leaf_cap) return fail(YK_ERR_UNSUPPORTED, "BVH leaf size above the kernel's leaf capacity");
   const ykbvh::Built bvh = ykbvh::build(centers.data(), radii.data(), count, cam_ext, opt);
@@ -3266,6 +3306,24 @@ int upload_tree(ykgpu_context* ctx, DevTree& t, const std::vector<double>& cente
       const uint32_t fit = used + min_stacks <= budget ? (uint32_t)((budget - used) / (rays * 4)) : 12u;
       pl.stack_cap = std::max(8u, std::min(3 * wdepth + 1, fit - 4));
       pl.stack_entries = pl.stack_cap + 4;
+      pl.stack_check = true;
+      // The FP64 branch-free visit (exact_stack) with 3 * wdepth + 1 entries: a visit at inner
+      // level k finds at most 3 entries per ancestor level on the stack (depth-first: what is left
+      // of an ancestor's up to 3 pushes; the sentinel is entry 0), so its top is <= 3k + 1 <=
+      // 3 * wdepth - 2, its writes (at the top and the next two entries) stay below entry
+      // 3 * wdepth and its new top is <= 3 * wdepth + 1: no overflow, no check, no slack
+      if (exact_stack && fit >= 3 * wdepth + 1) {
+        pl.stack_cap = 3 * wdepth + 1;
+        pl.stack_entries = pl.stack_cap;
+        pl.stack_check = false;
+      }
+#ifdef YK_STACK_CAP_FORCE
+      // (test builds, tests/test_gpu_robust.py: a checked stack this shallow overflows, and the
+      // lanes that overflow take the exact linear scan)
+      pl.stack_cap = YK_STACK_CAP_FORCE;
+      pl.stack_entries = pl.stack_cap + 4;
+      pl.stack_check = true;
+#endif
     }
     pl.tgeo_off = pl.in_lds && tgeo_elem ? (uint32_t)scene_bytes : 0u;
     pl.mat_off = pl.in_lds && tgeo_elem ? (uint32_t)(scene_bytes + tgeo_bytes) : 0u;
@@ -3447,7 +3505,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   const RenderKernel k64[2][2] = {{fp64_kernel(false, 0), fp64_kernel(true, 0)},
                                   {fp64_kernel(false, 4), fp64_kernel(true, 4)}};
   int rc = upload_tree(ctx, ctx->t64, centers, radii, cam_ext, bopt, kLeafCapF64, geo.data(), sizeof(SphereGeo),
-                       sizeof(SphereGeo), k64);
+                       sizeof(SphereGeo), k64, YK_NODE_BF != 0 && YK_STACK_EXACT != 0);
   if (rc) return rc;
   ykbvh::Options fopt = bopt;
   fopt.max_leaf = kLeafCapF32;  // the FP32 kernel's leaf loop is unrolled for two spheres
@@ -3457,7 +3515,7 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
   const RenderKernel k32[2][2] = {{f32_kernel(false, 0), f32_kernel(true, 0)},
                                   {f32_kernel(false, 4), f32_kernel(true, 4)}};
   rc = upload_tree(ctx, ctx->t32, centers, radii, cam_ext, fopt, kLeafCapF32, geo_f.data(), sizeof(float4),
-                   sizeof(float4), k32);
+                   sizeof(float4), k32, false);
   if (rc) return rc;
   // the float bound assumes neither underflow nor overflow: a scene outside that
   // scale renders FP32 with the linear scan throughout
