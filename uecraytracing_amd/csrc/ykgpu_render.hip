@@ -150,6 +150,15 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 #define YK_STACK_EXACT 1
 #endif
 
+// the FP64 unwind without the spill check when no ending lane of the wave spilled, two ids per
+// round (bench 156.6 -> 156.0 ms, profiles/r06_ab/unwind/; 0: the round-5 unwind, A/B)
+#ifndef YK_UNWIND_FAST
+#define YK_UNWIND_FAST 1
+#endif
+// slot claims: the tail size from a kernel argument and the leader's counter by v_readlane (A/B)
+#ifndef YK_CLAIM_ARGS
+#define YK_CLAIM_ARGS 0
+#endif
 #ifndef YK_CLAIM
 #define YK_CLAIM 512
 #endif
@@ -227,7 +236,8 @@ struct KernelArgs {
   unsigned long long* counters;  // [segments, sphere_tests, sqrt_calls, mt_fallbacks, nodes]
   double* trace;                 // YK_FLAG_TRACE_RAYS: rays [(q*spp + s)*trace_cap + k][6]
   uint32_t* trace_counts;        //   ray_color calls per sample [q*spp + s]
-  uint32_t trace_cap, pad_t;
+  uint32_t trace_cap;
+  uint32_t claim_tail;  // slots left below which a wave claims kClaimTail: grid x waves x kClaim x factor
   unsigned long long* clk;  // this launch's shader-clock probe (YK_CLOCK_*): 4 words
   // the tile's columns (include/ykgpu.h yk_render_params; the whole width: Wt = W, 0, 1, 0)
   uint32_t Wt, col_begin, col_stride, col_band;
@@ -865,12 +875,20 @@ __device__ __forceinline__ bool claim_slots(const KernelArgs& ka, bool in_path, 
       if (kClaimTail) {
         // res_base + res_left: where the counter stood after this wave's last claim
         const uint32_t seen = res_base + res_left;
+#if YK_CLAIM_ARGS
+        const uint32_t tail = ka.claim_tail;  // (the host's: no dispatch-packet load, no vmcnt wait)
+#else
         const uint32_t tail = gridDim.x * (blockDim.x >> 6) * kClaim * kClaimTailFactor;
+#endif
         if (seen >= ka.nsl || ka.nsl - seen < tail) csize = kClaimTail;
       }
       const int leader = __ffsll((long long)m) - 1;
       if ((int)lane == leader) fresh = atomicAdd(ka.pixel_counter, csize);
+#if YK_CLAIM_ARGS
+      fresh = __builtin_amdgcn_readlane(fresh, leader);  // (the leader is wave-uniform)
+#else
       fresh = __shfl(fresh, leader);
+#endif
     }
     if (!in_path) {
       const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
@@ -1526,6 +1544,26 @@ void yk_render_persistent(KernelArgs ka) {
         --nstk;
         return id;
       };
+#if YK_UNWIND_FAST
+      if (__ballot(nstk > kStackRegs) == 0) {
+        // no ending lane of the wave holds spilled ids: the register window alone, two ids per
+        // round (the window moves by a whole register)
+        while (nstk > 0) {
+          const SphereMat m = mat[st0 & 0xffffu];
+          L_r = m.ar * L_r;
+          L_g = m.ag * L_g;
+          L_b = m.ab * L_b;
+          if (nstk > 1) {
+            const SphereMat m2 = mat[st0 >> 16];
+            L_r = m2.ar * L_r;
+            L_g = m2.ag * L_g;
+            L_b = m2.ab * L_b;
+          }
+          st0 = st1, st1 = st2, st2 = st3;
+          nstk = nstk > 1 ? nstk - 2 : 0;
+        }
+      } else
+#endif
       while (nstk > 0) {
         const SphereMat m = mat[pop()];
         L_r = m.ar * L_r;
@@ -2880,7 +2918,7 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   ka.trace = ctx->d_trace;
   ka.trace_counts = ctx->d_trace_counts;
   ka.trace_cap = ctx->trace_cap;
-  ka.pad_t = 0;
+  ka.claim_tail = (uint32_t)grid * (uint32_t)(block / 64) * kClaim * kClaimTailFactor;
   if ((ka.flags & YK_FLAG_TRACE_RAYS) && !(ctx->d_trace && (ka.flags & YK_FLAG_COUNT_WORK)))
     return fail(YK_ERR_INVALID, "YK_FLAG_TRACE_RAYS is set by ykgpu_render_trace only");
   WarmArgs wa;
