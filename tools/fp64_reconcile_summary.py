@@ -38,7 +38,7 @@ def main():
                     "lane_util": round(c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"]), 3)})
     rc = json.load(open(os.path.join(d, "rec_counts.json")))
     ren = [c for n, c in per_dispatch(os.path.join(d, "rec", "run_counter_collection.csv"))
-           if "yk_render_persistent" in n]
+           if "yk_render_persistent" in n or "yk_render_counting" in n]
     assert len(ren) == 2, "expected two render dispatches (all lanes, one lane)"
     st = rc["calls"][0]
     assert all(rc["calls"][1][k] == st[k] for k in st if k != "flags"), "calls did different work"

@@ -70,6 +70,7 @@ DEFER_BUILD = os.environ.get("YK_DEFER_MODEL", "k4")
 P_REJECT = 1.0 - 3.141592653589793 / 4.0
 
 RENDER = "yk_render_persistent<true, "
+COUNTING = "yk_render_counting<true, "  # the counting instances (round 6: a kernel name of their own)
 WARM = "yk_mt_warmup"  # yk_mt_warmup<true, false> or yk_mt_warmup_defer
 
 
@@ -123,9 +124,9 @@ def main():
     st = next(c for c in pr["calls"] if c["call"] == "B")
     n = st["samples"]
     disp = dispatches(pmc_dir)
-    # render: production (A) is <true, 0>; B and C are both <true, 1>
+    # render: production (A) is yk_render_persistent<true, 0>; B and C are both yk_render_counting<true, 1>
     ra = per_call(disp, RENDER + "0>", 1)[0]
-    rb, rc = per_call(disp, RENDER + "1>", 2)
+    rb, rc = per_call(disp, COUNTING + "1>", 2)
     wa, wb, wc = per_call(disp, WARM, 3)
     e_a, lu_a = executed(ra)
     e_b, lu_b = executed(rb)

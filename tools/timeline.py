@@ -8,7 +8,7 @@ rows = [r for r in csv.DictReader(open(sys.argv[1]))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 want = int(sys.argv[2]) if len(sys.argv) > 2 else -1
 # calls: a call starts with a warm-up that follows a reduce with ra.last (group by gaps > 5 ms)
-kinds = {"yk_mt_warmup": "W", "yk_render_persistent": "R", "yk_render_f32": "R", "yk_reduce_samples": "S"}
+kinds = {"yk_mt_warmup": "W", "yk_render_persistent": "R", "yk_render_counting": "R", "yk_render_f32": "R", "yk_reduce_samples": "S"}
 ev = []
 for r in rows:
     k = next((v for n, v in kinds.items() if n in r["Kernel_Name"]), None)

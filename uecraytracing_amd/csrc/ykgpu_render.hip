@@ -110,8 +110,10 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #define YK_RENDER_PRIO 1
 #endif
 // the visit's slab constants as one op_sel-read register pair per axis and bound (yk_slab.hpp):
-// FP64 123 -> 115 VGPRs and no faster (512 spp 173.9 -> 174.2 ms: the FP64 kernel keeps the
-// broadcast pairs); FP32 125 -> 111 VGPRs and faster (195.3 -> 190.1 ms, profiles/r04_ab/f32/).
+// round 4: FP64 123 -> 115 VGPRs and no faster (512 spp 173.9 -> 174.2 ms), FP32 125 -> 111 VGPRs
+// and faster (195.3 -> 190.1 ms, profiles/r04_ab/f32/).  Round 6, on the branch-free visit: FP64
+// 128 -> 114 VGPRs, bench -0.7% (the SIMD's spare registers take a third warm-up wave,
+// profiles/r06_ab/vgpr/), so both kernels now read slab pairs.
 // YK_SLAB_PAIRS sets both (A/B).  (Round 4's two-paths-per-lane kernel, which lost its A/B, is
 // kept as a patch beside its evidence: profiles/r04_ab/dual/yk_dual.patch.)
 #ifdef YK_SLAB_PAIRS
@@ -119,7 +121,7 @@ constexpr int block_of(bool x128) { return x128 ? kBlockX128 : kBlock; }
 #define YK_SLAB_PAIRS_F32 YK_SLAB_PAIRS
 #endif
 #ifndef YK_SLAB_PAIRS_F64
-#define YK_SLAB_PAIRS_F64 0
+#define YK_SLAB_PAIRS_F64 1
 #endif
 #ifndef YK_SLAB_PAIRS_F32
 #define YK_SLAB_PAIRS_F32 1
@@ -155,9 +157,16 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 #ifndef YK_UNWIND_FAST
 #define YK_UNWIND_FAST 1
 #endif
-// slot claims: the tail size from a kernel argument and the leader's counter by v_readlane (A/B)
+// slot claims: the tail size from a kernel argument and the leader's counter by v_readlane (the
+// claim's bookkeeping becomes scalar: 2 VGPRs fewer; 0: A/B)
 #ifndef YK_CLAIM_ARGS
-#define YK_CLAIM_ARGS 0
+#define YK_CLAIM_ARGS 1
+#endif
+// VGPRs of the production FP64 render instances: 3 render waves x 112 of a SIMD's 512 leave 176, three
+// 48-VGPR warm-up waves and a reduce wave (bench -0.4% against the natural 114 -> 120; 104 spills
+// and starves the render: +3.4%, profiles/r06_ab/vgpr/); the counting instances keep theirs
+#ifndef YK_RENDER_VGPRS
+#define YK_RENDER_VGPRS 112
 #endif
 #ifndef YK_CLAIM
 #define YK_CLAIM 512
@@ -921,18 +930,7 @@ using RenderKernel = void (*)(KernelArgs);
 // the hash's 64-bit arithmetic and two more kernel arguments cost the counter-seeded production
 // instance 0.6% through SGPR spills); bit 2: the yk::xor128 engine (YK_RNG_XOR128)
 template <bool kSceneInLds, int kMode>
-__global__ __launch_bounds__(mode_block<kMode>())
-#if YK_WAVES_PER_EU
-__attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
-#else
-// production instances at <= 128 VGPRs (one short of their natural 129): 3 x 128 of a SIMD's 512
-// leave 128, four yk_mt_warmup waves of 32 (the counting instances keep their registers)
-__attribute__((amdgpu_waves_per_eu((kMode & 1) ? 1 : 4, 8)))
-#endif
-#ifdef YK_SINGLE_VGPRS
-__attribute__((amdgpu_num_vgpr(YK_SINGLE_VGPRS / 2)))  // (A/B; gfx950 counts the unified file: x2)
-#endif
-void yk_render_persistent(KernelArgs ka) {
+__device__ __forceinline__ void render_body(KernelArgs ka) {
   constexpr int kBlk = mode_block<kMode>();
   constexpr bool kCount = (kMode & 1) != 0;
   constexpr bool kRandomSeed = (kMode & 2) != 0;
@@ -1608,15 +1606,41 @@ void yk_render_persistent(KernelArgs ka) {
 #endif
 }
 
+
+// The kernels.  Production instances at <= YK_RENDER_VGPRS (gfx950's amdgpu_num_vgpr counts the
+// unified file, so the attribute takes half).
+template <bool kSceneInLds, int kMode>
+__global__ __launch_bounds__(mode_block<kMode>())
+#if YK_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(YK_WAVES_PER_EU, YK_WAVES_PER_EU)))
+#else
+__attribute__((amdgpu_waves_per_eu(4, 8)))
+#endif
+#ifdef YK_SINGLE_VGPRS
+__attribute__((amdgpu_num_vgpr(YK_SINGLE_VGPRS / 2)))  // (A/B)
+#else
+__attribute__((amdgpu_num_vgpr(YK_RENDER_VGPRS / 2)))
+#endif
+void yk_render_persistent(KernelArgs ka) {
+  render_body<kSceneInLds, kMode>(ka);
+}
+// the counting instances (kMode bit 0: diagnostic builds of the same body, YK_FLAG_COUNT_WORK)
+// under a name of their own, their registers uncapped
+template <bool kSceneInLds, int kMode>
+__global__ __launch_bounds__(mode_block<kMode>()) __attribute__((amdgpu_waves_per_eu(1, 8)))
+void yk_render_counting(KernelArgs ka) {
+  render_body<kSceneInLds, kMode>(ka);
+}
+
 // The FP64 instance for (scene in LDS, kMode)
 RenderKernel fp64_kernel(bool lds, int mode) {
   static const RenderKernel k[16] = {
-      yk_render_persistent<false, 0>, yk_render_persistent<false, 1>, yk_render_persistent<false, 2>,
-      yk_render_persistent<false, 3>, yk_render_persistent<false, 4>, yk_render_persistent<false, 5>,
-      yk_render_persistent<false, 6>, yk_render_persistent<false, 7>, yk_render_persistent<true, 0>,
-      yk_render_persistent<true, 1>,  yk_render_persistent<true, 2>,  yk_render_persistent<true, 3>,
-      yk_render_persistent<true, 4>,  yk_render_persistent<true, 5>,  yk_render_persistent<true, 6>,
-      yk_render_persistent<true, 7>};
+      yk_render_persistent<false, 0>, yk_render_counting<false, 1>,  yk_render_persistent<false, 2>,
+      yk_render_counting<false, 3>,   yk_render_persistent<false, 4>, yk_render_counting<false, 5>,
+      yk_render_persistent<false, 6>, yk_render_counting<false, 7>,  yk_render_persistent<true, 0>,
+      yk_render_counting<true, 1>,    yk_render_persistent<true, 2>,  yk_render_counting<true, 3>,
+      yk_render_persistent<true, 4>,  yk_render_counting<true, 5>,    yk_render_persistent<true, 6>,
+      yk_render_counting<true, 7>};
   return k[(lds ? 8 : 0) + (mode & 7)];
 }
 
