@@ -429,5 +429,10 @@ __device__ __forceinline__ double reflectance(double cosine, double ref_idx) {
   const double x = 1 - cosine;
   return r0 + (1 - r0) * ((((x * x) * x) * x) * x);
 }
+// the same from r0 = ((1 - ref_idx) / (1 + ref_idx))^2 computed ahead (per material and side)
+__device__ __forceinline__ double reflectance_r0(double cosine, double r0) {
+  const double x = 1 - cosine;
+  return r0 + (1 - r0) * ((((x * x) * x) * x) * x);
+}
 
 }  // namespace ykd

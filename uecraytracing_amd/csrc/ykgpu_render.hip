@@ -152,6 +152,11 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 #define YK_STACK_EXACT 1
 #endif
 
+// the FP64 dielectric's 1/ior and Schlick r0 (both sides) precomputed on the host: two FP64
+// divisions fewer per trip with a glass hit (bench -0.6%, profiles/r06_ab/shade/; 0: A/B)
+#ifndef YK_DIEL_PRE
+#define YK_DIEL_PRE 1
+#endif
 // the FP64 unwind without the spill check when no ending lane of the wave spilled, two ids per
 // round (bench 156.6 -> 156.0 ms, profiles/r06_ab/unwind/; 0: the round-5 unwind, A/B)
 #ifndef YK_UNWIND_FAST
@@ -1494,7 +1499,14 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
         } else {  // dielectric extension (attenuation (1,1,1): multiplying by 1.0 is exact)
           if (kCount) ++n_diel;
           push = false;
+#if YK_DIEL_PRE
+          // 1/ior and Schlick's r0 of both sides precomputed on the host with the same IEEE
+          // operations (ykgpu_set_scene: the dielectric's unused fuzz / albedo fields)
+          const double ratio = front ? m.fuzz : m.ior;
+          const double r0 = front ? m.ar : m.ag;
+#else
           const double ratio = front ? (1.0 / m.ior) : m.ior;
+#endif
           const v3 unit = un;
           const double sn = sq2;
           const bool cannot = ratio * sn > 1.0;
@@ -1504,7 +1516,11 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
           } else {
             u = spec ? ykd::uniform_of(c0, 0, 1) : ykd::uniform(g, 0, 1);
           }
+#if YK_DIEL_PRE
+          if (cannot || ykd::reflectance_r0(ct, r0) > u) {
+#else
           if (cannot || ykd::reflectance(ct, ratio) > u) {
+#endif
             nd = ykd::reflect(unit, nrm);
           } else {
             const v3 perp = ykd::mul(ykd::add(unit, ykd::mul(nrm, ct)), ratio);
@@ -3521,6 +3537,20 @@ int ykgpu_set_scene(ykgpu_context* ctx, const yk_sphere* spheres, uint32_t count
     const float rf = (float)s.radius;
     geo_f[i] = make_float4((float)s.center[0], (float)s.center[1], (float)s.center[2], rf * rf);
     mat[i] = {s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.radius, s.ior, s.material, 0.0f, 0.0};  // inv_r*: yk_mat_prep
+#if YK_DIEL_PRE
+    if (s.material == YK_MATERIAL_DIELECTRIC) {
+      // the FP64 kernel's dielectric reads 1/ior and Schlick's r0 for both sides of the surface
+      // from its otherwise unused fields (never unwound: its attenuation is 1), computed here
+      // with the operations and order of ykd::reflectance (IEEE double, no contraction)
+      const double inv = 1.0 / s.ior;
+      double r0f = (1 - inv) / (1 + inv), r0b = (1 - s.ior) / (1 + s.ior);
+      r0f = r0f * r0f;
+      r0b = r0b * r0b;
+      mat[i].fuzz = inv;
+      mat[i].ar = r0f;
+      mat[i].ag = r0b;
+    }
+#endif
   }
   YK_HIP(hipSetDevice(ctx->device));
   // a render enqueued by ykgpu_render_async on the caller's stream (and its launches on the
