@@ -5,14 +5,15 @@
 // samples → to_color3b) and the recursion of yk/raytracer.hpp:19-37.
 //
 // Execution model:
-//   * a render call is a sequence of LAUNCHES of K samples per pixel (4, 8, 16, then at most
-//     kmax = kLaunchSpp = 32 for the frame: 1920x1080x512 is 4, 8, 16, 14 x 32, 18, 18; a call
-//     enqueued while the previous one still runs: 16 x 32).  Per launch: yk_mt_warmup (second
+//   * a render call is a sequence of LAUNCHES of K samples per pixel (a synced call: 4, 8, 16,
+//     then at most kLaunchSpp = 32 for the frame: 1920x1080x512 is 4, 8, 16, 14 x 32, 18, 18; a
+//     call enqueued while the previous one still runs: kLaunchSppOv = 64, 8 x 64).  Per launch: yk_mt_warmup (second
 //     stream: every sample's mt19937 seeding walk and its start draws — jitter and lens — and
 //     camera ray, as a StartRec), yk_render_persistent (the paths, on one of two top-priority
 //     streams), yk_reduce_samples (the reference's strictly sequential per-pixel sum and
 //     to_color3b, third stream).  Back-to-back calls overlap (launches numbered across calls).
-//   * yk_render_persistent is one persistent grid of 768-thread workgroups, one per CU, with
+//   * yk_render_persistent is one persistent grid of 768-thread workgroups, one per CU (12 waves,
+//     3 per SIMD at 112 VGPRs, beside three 48-VGPR warm-up waves), with
 //     the scene (BVH, geometry and material tables) in LDS, over SAMPLE SLOTS: a lane runs one path at a
 //     time, one SEGMENT (closest hit + scatter) per trip round the loop, writes the sample's
 //     colour when the path ends and takes the next slot from a wave-level reserve (one atomic
@@ -2525,6 +2526,16 @@ static_assert(kLaunchBytes / (8 * kColStride) * 4 < (1ull << 32), "4 * slot must
 #define YK_LAUNCH_SPP 32
 #endif
 constexpr uint32_t kLaunchSpp = YK_LAUNCH_SPP;
+// ... and for a call enqueued while the previous one still runs (launch() `inflight`): its launches
+// need no ramp and overlap the calls around them, so the per-launch handover is what is left, and
+// half as many launches pay it (frame: 8 of 64 instead of 16 of 32: bench -1.7%); a synced call
+// keeps kLaunchSpp (64 there cost it 2%: the 64-spp warm-up under the ramp's 32-spp render and a
+// longer last launch alone on the device, profiles/r06_ab/shade/).  The rings hold the larger
+// launch in both, so a synced call and the in-flight calls after it share one ring geometry.
+#ifndef YK_LAUNCH_SPP_OV
+#define YK_LAUNCH_SPP_OV 64
+#endif
+constexpr uint32_t kLaunchSppOv = YK_LAUNCH_SPP_OV;
 // ... or spp / kLaunchesPerCall when that is more (a long call: launch())
 #ifndef YK_LAUNCHES_PER_CALL
 #define YK_LAUNCHES_PER_CALL 32
@@ -2569,6 +2580,11 @@ constexpr uint32_t kFirstLaunch = YK_FIRST_LAUNCH;  // samples per pixel in the 
 #define YK_SCHED_GROW 2
 #endif
 constexpr uint32_t kSchedGrow = YK_SCHED_GROW;
+// ... and by half from this many samples per pixel on (0: kSchedGrow throughout)
+#ifndef YK_SCHED_SLOW
+#define YK_SCHED_SLOW 0
+#endif
+constexpr uint32_t kSchedSlow = YK_SCHED_SLOW;
 // ... and for a call enqueued while the previous one still runs (launch(): `inflight`): every
 // launch at kmax (YK_FIRST_LAUNCH_OV 0; else that many samples per pixel first, growing by
 // YK_SCHED_GROW_OV)
@@ -2648,6 +2664,9 @@ hipError_t create_render_stream(hipStream_t* s) {
 // and 2 holds 4.2 GB less at the headline size (call_bytes 22.3 -> 18.1 GB)
 #ifndef YK_COL_RING
 #define YK_COL_RING 2
+#endif
+#ifndef YK_RED_PRIO
+#define YK_RED_PRIO 0
 #endif
 uint32_t col_ring() {
   uint32_t r = YK_COL_RING;
@@ -2749,9 +2768,14 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // ~64 GB (3 x 2.07M x 121 x 64 B of start records, 2 x 2.07M x 121 x 32 B of colours).
   uint64_t launch_spp = std::max<uint64_t>(kLaunchSpp, spp / kLaunchesPerCall);
   if (const char* e = ab_knob("YKGPU_LAUNCH_SPP")) launch_spp = (uint64_t)std::max(1, std::atoi(e));  // (A/B)
-  const uint32_t kideal = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
-                             std::max<uint64_t>({launch_spp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
+  const uint64_t launch_spp_ov = std::max<uint64_t>(std::max<uint64_t>(kLaunchSppOv, launch_spp), spp / kLaunchesPerCall);
+  auto ideal_for = [&](uint64_t lspp) {
+    return (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
+                               std::max<uint64_t>({lspp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
+  };
+  // the rings' launch size (an in-flight call's launches) and a synced call's, <= it
+  const uint32_t kideal = ideal_for(launch_spp_ov), ksynced = ideal_for(launch_spp);
   // A device short of memory (other contexts, other processes) makes the call slower, not fatal:
   // the rings are sized for launches of kmax samples per pixel, and when the device cannot hold
   // them — free memory (hipMemGetInfo) plus what this context's rings already hold, or a
@@ -2800,6 +2824,8 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     if (ctx->prev_enqueued && ctx->prev_ok && !ctx->dirty && ctx->prev_shape == shape && ctx->prev_n > 0 &&
         ctx->lev.size() >= 6ull * ctx->prev_n)
       inflight = hipEventQuery(ctx->lev[6 * (ctx->prev_n - 1) + 5]) == hipErrorNotReady;
+    // this call's largest launch: the rings' (kmax) in flight, a synced call's own below it
+    const uint32_t kcap = inflight ? kmax : std::min(kmax, ksynced);
     uint32_t first_k = inflight ? (kFirstLaunchOv ? kFirstLaunchOv : kmax) : kFirstLaunch;
     uint32_t grow_k = inflight ? kSchedGrowOv : kSchedGrow;
     if (const char* e = ab_knob(inflight ? "YKGPU_FIRST_LAUNCH_OV" : "YKGPU_FIRST_LAUNCH"))
@@ -2815,14 +2841,17 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     // aligned: at 32 spp its grid-stride is the pixel count, so a lane's four walks are four
     // samples of one pixel (their processing-order reads coincide; a 30- or 31-spp launch fetches
     // 1.7x the bytes per slot in the warm-up, profiles/r06_ab/pmc/)
-    for (uint32_t s0 = 0, k = std::min(first_k, kmax); s0 < spp;) {
+    for (uint32_t s0 = 0, k = std::min(first_k, kcap); s0 < spp;) {
       uint32_t take = std::min(k, spp - s0);
       const uint32_t rest = spp - (s0 + take);
       if (rest > 0 && rest < std::max(1u, take / 4))
-        take = spp - s0 <= kmax ? spp - s0 : (spp - s0 + 1) / 2;
+        take = spp - s0 <= kcap ? spp - s0 : (spp - s0 + 1) / 2;
       sched.emplace_back(s0, take);
       s0 += take;
-      k = std::min(grow_k * k, kmax);
+      // past kSchedSlow spp the ramp grows by half: a warm-up twice its render's size no longer
+      // hides under it (64-spp launches: the 64-spp warm-up under the 32-spp render cost the
+      // synced call 2%, profiles/r06_ab/shade/r06z_*)
+      k = std::min(kSchedSlow && k >= kSchedSlow ? k + k / 2 : grow_k * k, kcap);
     }
     // a launch buffer of the rings holds kmax samples per pixel (every launch fits: above)
     K = kmax;
@@ -3476,7 +3505,11 @@ int ykgpu_context_create(int device, ykgpu_context** out) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
+#if YK_RED_PRIO
+      create_render_stream(&ctx->red) != hipSuccess ||  // (A/B: the reduces at the renders' priority)
+#else
       hipStreamCreateWithFlags(&ctx->red, hipStreamNonBlocking) != hipSuccess ||
+#endif
       create_render_stream(&ctx->alt) != hipSuccess || create_render_stream(&ctx->ren) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
       hipMalloc(&ctx->d_stats, kCounters * sizeof(unsigned long long)) != hipSuccess) {
