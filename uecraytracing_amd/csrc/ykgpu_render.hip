@@ -2551,6 +2551,13 @@ constexpr uint32_t kLaunchesPerCall = YK_LAUNCHES_PER_CALL;
 #define YK_LAUNCH_SLOTS (1u << 26)
 #endif
 constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
+// ... and of about kLaunchSlotsOv for an in-flight call (as kLaunchSppOv for the frame), never
+// fewer than two launches where a synced call has two: the 4-way tile 38.73 -> 38.59 ms, the 2-way
+// 76.73 -> 76.18, config 4's 8-way 153.78 -> 153.10, the 8-way unchanged (profiles/r06_ab/tiles/r06ae_*)
+#ifndef YK_LAUNCH_SLOTS_OV
+#define YK_LAUNCH_SLOTS_OV (1u << 27)
+#endif
+constexpr uint64_t kLaunchSlotsOv = YK_LAUNCH_SLOTS_OV;
 // global launch numbers whose dependency events (ykgpu_context::gev) are kept: more than any ring
 // is deep
 constexpr uint32_t kDepRing = 16;
@@ -2758,8 +2765,15 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   const uint64_t fill_spp = ((uint64_t)grid * block * 16 + nps - 1) / nps;
   uint64_t launch_slots = kLaunchSlots;  // (A/B knob: YKGPU_LAUNCH_SLOTS)
   if (const char* e = ab_knob("YKGPU_LAUNCH_SLOTS")) launch_slots = (uint64_t)std::max(1ll, std::atoll(e));
-  const uint64_t call_launches = std::max<uint64_t>(1, ((uint64_t)nps * spp + launch_slots / 2) / launch_slots);
+  auto launches_for = [&](uint64_t lslots) {
+    return std::max<uint64_t>(1, ((uint64_t)nps * spp + lslots / 2) / lslots);
+  };
+  // (in flight: never fewer than two launches where a synced call has two — a one-launch call has
+  // rings of one buffer and overlaps nothing: the 8-way tile 19.6 -> 25.5 ms, r06ad)
+  const uint64_t call_launches = launches_for(launch_slots);
+  const uint64_t call_launches_ov = std::max(std::min<uint64_t>(call_launches, 2), launches_for(std::max(launch_slots, kLaunchSlotsOv)));
   const uint64_t slot_spp = (spp + call_launches - 1) / call_launches;
+  const uint64_t slot_spp_ov = (spp + call_launches_ov - 1) / call_launches_ov;
   // A long call takes longer launches: every launch pays a drain whose length is the longest path
   // of its last samples, and many launches per call buy nothing once there are ~32 (config 5,
   // 1920x1080x4096 at depth 200 on the glass scene: 32 spp per launch 1730 ms, 64 1631, 121 (the
@@ -2769,13 +2783,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   uint64_t launch_spp = std::max<uint64_t>(kLaunchSpp, spp / kLaunchesPerCall);
   if (const char* e = ab_knob("YKGPU_LAUNCH_SPP")) launch_spp = (uint64_t)std::max(1, std::atoi(e));  // (A/B)
   const uint64_t launch_spp_ov = std::max<uint64_t>(std::max<uint64_t>(kLaunchSppOv, launch_spp), spp / kLaunchesPerCall);
-  auto ideal_for = [&](uint64_t lspp) {
+  auto ideal_for = [&](uint64_t lspp, uint64_t sspp) {
     return (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>({spp, kLaunchBytes / (8ull * kColStride * nps),
-                               std::max<uint64_t>({lspp, fill_spp, slot_spp}), ((1ull << 31) - 1) / nps}));
+                               std::max<uint64_t>({lspp, fill_spp, sspp}), ((1ull << 31) - 1) / nps}));
   };
   // the rings' launch size (an in-flight call's launches) and a synced call's, <= it
-  const uint32_t kideal = ideal_for(launch_spp_ov), ksynced = ideal_for(launch_spp);
+  const uint32_t kideal = ideal_for(launch_spp_ov, slot_spp_ov), ksynced = ideal_for(launch_spp, slot_spp);
   // A device short of memory (other contexts, other processes) makes the call slower, not fatal:
   // the rings are sized for launches of kmax samples per pixel, and when the device cannot hold
   // them — free memory (hipMemGetInfo) plus what this context's rings already hold, or a
