@@ -197,43 +197,44 @@ def test_shallow_checked_stack_overflows_to_the_linear_scan():
 
 
 def test_two_and_three_launch_calls_back_to_back():
-    """Calls of an 8-way column tile of 1920x1080 (259,200 pixels): 512 spp is two launches of 256
-    spp and 768 spp three (launches of ~2^26 slots), with launch buffers of kmax = 256
-    either way, so the rings (three start-record buffers, two colour buffers) are deeper than a
-    two-launch call and every call reuses buffers of the calls before it (ctx->gev, run_len).
-    Enqueued back to back in a mixed order, every image equals the synced render of its params,
-    and two rows equal the CPU oracle's."""
+    """Calls of an 8-way column tile of 1920x1080 (259,200 pixels): in flight, 1024 spp is two
+    launches of 512 spp and 1536 spp three (launches of ~2^27 slots), so both calls have
+    rings of kmax = 512 — three start-record buffers and two colour buffers, deeper than a
+    two-launch call — and every call reuses buffers of the calls before it (ctx->gev, run_len); a
+    synced call spreads its samples over launches of ~2^26 slots inside the same rings.  Enqueued
+    back to back in a mixed order, every image equals the synced render of its params, and two rows
+    equal the CPU oracle's."""
     torch = pytest.importorskip("torch")
     from uecraytracing_amd.tiles import rank_tile
     arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
     with yk.Renderer(0) as r:
         r.set_scene(arr, cam)
         tk = rank_tile(3, 8, 1080, 1920, "cols")
-        p2 = make_params(1920, 1080, 512, 50, 404, **tk)
-        p3 = make_params(1920, 1080, 768, 50, 404, **tk)
-        want = {512: r.render(p2), 768: r.render(p3)}
+        p2 = make_params(1920, 1080, 1024, 50, 404, **tk)
+        p3 = make_params(1920, 1080, 1536, 50, 404, **tk)
+        want = {1024: r.render(p2), 1536: r.render(p3)}
         st = r.stats()
-        assert st["launch_spp"] == 256
-        seq = [p2, p2, p3, p2, p3, p3, p2]
+        assert st["launch_spp"] == 512 and st["launches"] > 3  # synced: ~2^26-slot launches in rings of 512
+        seq = [p2, p2, p3, p2, p3, p2, p3]
         outs = [torch.zeros((1080, p2.tile_width(), 3), dtype=torch.uint8, device="cuda:0") for _ in seq]
         torch.cuda.synchronize()
         s = torch.cuda.Stream()
         for p, o in zip(seq, outs):  # no synchronisation between the calls
             r.render_async(p, o.data_ptr(), s.cuda_stream)
         s.synchronize()
-        st = r.stats()  # the last call's: in flight, two launches at kmax
-        assert st["launches"] == 2 and st["launch_spp"] == 256
+        st = r.stats()  # the last call's: in flight, three launches at kmax
+        assert st["launches"] == 3 and st["launch_spp"] == 512
         for p, o in zip(seq, outs):
             np.testing.assert_array_equal(o.cpu().numpy(), want[p.samples_per_pixel])
     xs = [x for x in range(1920) if (x >> 3) % 8 == 3]
-    cpu, _, _, _ = oracle_lib.render(arr, cam, make_params(1920, 1080, 512, 50, 404, rows=(5, 2, 1070)), nthreads=16)
-    np.testing.assert_array_equal(want[512][[5, 1075]], cpu[:, xs])
+    cpu, _, _, _ = oracle_lib.render(arr, cam, make_params(1920, 1080, 1024, 50, 404, rows=(5, 2, 1070)), nthreads=16)
+    np.testing.assert_array_equal(want[1024][[5, 1075]], cpu[:, xs])
 
 
 def test_random_back_to_back_sequence_of_mixed_calls():
     """A seeded random sequence of calls enqueued back to back without synchronisation — whole
-    frames and row / column tiles of 1920x1080 whose in-flight launches are 1, 2 or 3 per call
-    (launches of ~2^26 slots), small single-launch calls, FP32 and xor128 calls between them — so
+    frames and row / column tiles of 1920x1080 whose launches are 1, 2 or 3 per call
+    (~2^26 slots synced, ~2^27 in flight), small single-launch calls, FP32 and xor128 calls between them — so
     calls of equal ring geometry overlap across calls of other geometries, of other launch counts
     and of other modes (launch(): ctx->gev, run_len).  Every output equals the synced render of its
     params."""
@@ -244,9 +245,9 @@ def test_random_back_to_back_sequence_of_mixed_calls():
     arr, cam = yk.read_scene(os.path.join(yk.SCENE_DIR, "final_seed42.yks"))
     shapes = [
         make_params(1920, 1080, 64, 50, 404),                                   # 2 launches of 32
-        make_params(1920, 1080, 96, 50, 404),                                   # 3 launches of 32
+        make_params(1920, 1080, 96, 50, 404),                                   # 3 of 32 synced, 2 of 48 in flight
         make_params(1920, 1080, 512, 50, 404, **rank_tile(2, 8, 1080, 1920, "rows")),   # 2 of 256
-        make_params(1920, 1080, 768, 50, 404, **rank_tile(2, 8, 1080, 1920, "rows")),   # 3 of 256
+        make_params(1920, 1080, 768, 50, 404, **rank_tile(2, 8, 1080, 1920, "rows")),   # 3 of 256 synced, 2 of 384 in flight
         make_params(1920, 1080, 256, 50, 404, **rank_tile(1, 4, 1080, 1920, "cols")),   # 2 of 128
         make_params(320, 180, 16, 50, 404),                                     # 1 launch
         make_params(320, 180, 16, 50, 404, precision=PRECISION_FP32),

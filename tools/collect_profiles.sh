@@ -7,8 +7,9 @@ S=gpurun_out/$T
 P=profiles
 cp $S/bench.json $P/${T}_bench.json
 cp $S/kt/run_kernel_stats.csv $P/${T}_kernel_stats.csv
-# (the kt run of gpu_profile_all.sh: 1 warm-up + 2 timed steps of 512 spp; the bench's launches are 32 spp)
-python3 tools/kernel_union.py $S/kt/run_kernel_trace.csv "yk_render_persistent<true, 0>" $P/${T}_kernel_union.json 1536 32 > /dev/null
+# (the kt run of gpu_profile_all.sh: 2 warm-up + 6 timed steps of 512 spp, the first of each synced; the
+# bench's in-flight launches are 64 spp, bench.py roofline.launch_ms)
+python3 tools/kernel_union.py $S/kt/run_kernel_trace.csv "yk_render_persistent<true, 0>" $P/${T}_kernel_union.json ${KT_SPP:-4096} 64 8 > /dev/null
 cp $S/pmc_summary.json $P/${T}_pmc_summary.json
 cp $S/pmc_summary.json $P/pmc_summary.json
 [ -f $S/pmc_summary_warmup.json ] && cp $S/pmc_summary_warmup.json $P/${T}_pmc_summary_warmup.json

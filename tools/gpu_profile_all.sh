@@ -17,5 +17,5 @@ cp gpurun_out/$T/pmc_hbm.json profiles/pmc_hbm.json
 timeout -k 10 400 python bench.py > gpurun_out/$T/bench.log 2>&1 || { echo BENCH_FAILED; tail -20 gpurun_out/$T/bench.log; exit 1; }
 grep '^{' gpurun_out/$T/bench.log | tail -1 > gpurun_out/$T/bench.json
 cat gpurun_out/$T/bench.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/kt -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-modes --no-configs --no-tiles > gpurun_out/$T/kt.log 2>&1 || { echo KT_FAILED; tail -20 gpurun_out/$T/kt.log; exit 2; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/kt -o run -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-modes --no-configs --no-tiles > gpurun_out/$T/kt.log 2>&1 || { echo KT_FAILED; tail -20 gpurun_out/$T/kt.log; exit 2; }
 echo done

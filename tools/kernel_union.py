@@ -6,11 +6,13 @@ twice.  This reports, for the dispatches whose name contains the substring: the 
 span (what --stats prints), the UNION of the spans, and union / dispatches — the figure bench.py
 divides by (`roofline.launch_ms`).
 usage: python tools/kernel_union.py <run_kernel_trace.csv> [kernel-substring[|substring...]] [out.json]
-                                    [spp_total spp_per_launch]
+                                    [spp_total spp_per_launch [last_launches]]
 With spp_total (every sample per pixel the traced run rendered with this kernel) and the bench's
 launch size, also union_per_launch_equiv_ms = union / (spp_total / spp_per_launch): the traced
-run mixes synced calls (launches of 4, 8, 16, 32 spp) and back-to-back ones (32 each), so this is
-the figure comparable with the bench's per-32-spp launch_ms.
+run mixes synced calls (launches of 4, 8, 16, 32 spp) and back-to-back ones (64 each, round 6), so
+this is the figure comparable with the bench's per-launch launch_ms.
+With last_launches, also union_last_call_per_launch_ms: the union of the last that many dispatches
+(the traced run's last call, in flight like the bench's timed steps after the first) / that many.
 Several substrings ('|'-separated) take the union of all their dispatches (kernels that share a
 launch); "launches" = the dispatches of the LAST substring (one per launch).
 """
@@ -47,6 +49,18 @@ def main():
         spp_total, per = float(sys.argv[4]), float(sys.argv[5])
         out["spp_total"], out["spp_per_launch"] = spp_total, per
         out["union_per_launch_equiv_ms"] = union / (spp_total / per) / 1e6
+    if len(sys.argv) > 6:
+        n = int(sys.argv[6])
+        last = iv[-n:]
+        u, (cs, ce) = 0, last[0]
+        for s_, e_ in last[1:]:
+            if s_ > ce:
+                u, cs, ce = u + ce - cs, s_, e_
+            else:
+                ce = max(ce, e_)
+        u += ce - cs
+        out["last_launches"] = n
+        out["union_last_call_per_launch_ms"] = u / n / 1e6
     js = json.dumps(out, indent=1)
     if len(sys.argv) > 3:
         open(sys.argv[3], "w").write(js + "\n")

@@ -149,6 +149,18 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 // the FP64 stack sized to the tree's proven depth (3 x wide depth + 1 entries) where LDS allows,
 // its overflow check then skipped (a scalar branch on KernelArgs::stack_check): bench 159.0 ->
 // 156.2 ms on top of YK_NODE_BF (0: always checked, A/B)
+// the FP64 visit's distances from tmin_lo, scaled by kClampScale, the near FMAs clamping to [0, 1]
+// in place of the max with tmin_lo (A/B)
+#ifndef YK_NEAR_CLAMP
+#define YK_NEAR_CLAMP 0
+#endif
+constexpr float kClampScale = 0x1p-24f;
+// the FP64 visit's slab min / max two slots per asm block (yk_slab.hpp slab_cull2): one hazard
+// pad per visit instead of eight, bench -0.2% (four of four same-box pairs, image hashes equal,
+// profiles/r06_ab/shade/r06ag_*)
+#ifndef YK_CULL_BLOCK
+#define YK_CULL_BLOCK 1
+#endif
 #ifndef YK_STACK_EXACT
 #define YK_STACK_EXACT 1
 #endif
@@ -1146,7 +1158,21 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
         // relative error inside the 2^-17 margin
         const float ixs = ix * kFar, iys = iy * kFar, izs = iz * kFar;
         const float ox_f = (float)o.x, oy_f = (float)o.y, oz_f = (float)o.z;
-#if YK_SLAB_PAIRS_F64
+        const float tmin_lo = __double2float_rd(ka.t_min) * (1.0f - 0x1p-17f);
+#if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
+        // Distances measured from tmin_lo and scaled by kClampScale = 2^-24: per
+        // axis (s/d, s(-o/d - tmin_lo)) (near) and (sc/d, s(-oc/d - tmin_lo)) (far).  The near
+        // FMAs clamp to [0, 1], which IS the max with tmin_lo (distances below 2^24 + tmin_lo
+        // never reach the clamp's 1; beyond, the clamp only lowers a near distance: more boxes
+        // kept, never fewer), so a slot costs max3 + min3 + min + compare.  s is a power of two
+        // (exact), the constants' subtraction one more rounding of the origin term
+        // (<= 2^-24 (|o/d| + t_min): inside the delta budget with the origin perturbation).
+        constexpr float kS = kClampScale;
+        const f2 sxp = {ix * kS, (-oix - tmin_lo) * kS}, syp = {iy * kS, (-oiy - tmin_lo) * kS},
+                 szp = {iz * kS, (-oiz - tmin_lo) * kS};
+        const f2 fxp = {ixs * kS, (-(ox_f * ixs) - tmin_lo) * kS}, fyp = {iys * kS, (-(oy_f * iys) - tmin_lo) * kS},
+                 fzp = {izs * kS, (-(oz_f * izs) - tmin_lo) * kS};
+#elif YK_SLAB_PAIRS_F64
         // per axis ONE register pair (1/d, -o/d) (near) and (c/d, -o c/d) (far), read by op_sel
         // (yk_slab.hpp): 12 VGPRs instead of 24
         const f2 sxp = {ix, -oix}, syp = {iy, -oiy}, szp = {iz, -oiz};
@@ -1159,10 +1185,15 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
                  noizc = {-(oz_f * izs), -(oz_f * izs)};
 #endif
         const double ia = ykd::rcp_bound(a);  // bounds only: relative error < 2^-44
-        const float tmin_lo = __double2float_rd(ka.t_min) * (1.0f - 0x1p-17f);
         double ustar = INFINITY;  // proven upper bound of the minimum exact root
-        float ustar_f = INFINITY;  // >= ustar * (1 + 2^-18)
+        float ustar_f = INFINITY;  // >= ustar * (1 + 2^-18) (YK_NEAR_CLAMP: >= s (that - tmin_lo))
+#if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
+        // a lane whose 1/d could leave float's normal range once scaled (|d| >= 1e30, never seen)
+        // is marked for the exact linear scan from the start (nc = 5, as an overflow)
+        uint32_t nc = dmax < 1e30f ? 0u : 5u, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#else
         uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#endif
         // candidate lower bounds kept as floats RN(L), compared with ustar_f >= RN(U*): by
         // monotone rounding (all bounds >= 0) L <= U* implies RN(L) <= ustar_f, so the float
         // comparison only ever keeps MORE candidates than the double comparison would
@@ -1220,19 +1251,46 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
             const int4 ch = *(const int4*)(nodes + node + 144);
 #endif
             bool hk[4];
-#if YK_SLAB_PAIRS_F64
+#if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
+            const f2 nx[2] = {slab_fma_clamp(qnx.xy, sxp), slab_fma_clamp(qnx.zw, sxp)};
+            const f2 fx[2] = {slab_fma(qfx.xy, fxp), slab_fma(qfx.zw, fxp)};
+            const f2 ny[2] = {slab_fma_clamp(qny.xy, syp), slab_fma_clamp(qny.zw, syp)};
+            const f2 fy[2] = {slab_fma(qfy.xy, fyp), slab_fma(qfy.zw, fyp)};
+            const f2 nz[2] = {slab_fma_clamp(qnz.xy, szp), slab_fma_clamp(qnz.zw, szp)};
+            const f2 fz[2] = {slab_fma(qfz.xy, fzp), slab_fma(qfz.zw, fzp)};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              float tna, tfa, tnb, tfb;
+              slab_cull2c(nx[h][0], ny[h][0], nz[h][0], fx[h][0], fy[h][0], fz[h][0], nx[h][1], ny[h][1], nz[h][1],
+                          fx[h][1], fy[h][1], fz[h][1], ustar_f, tna, tfa, tnb, tfb);
+              hk[2 * h] = tna <= tfa;
+              hk[2 * h + 1] = tnb <= tfb;
+            }
+#elif YK_SLAB_PAIRS_F64
             const f2 nx[2] = {slab_fma(qnx.xy, sxp), slab_fma(qnx.zw, sxp)};
             const f2 fx[2] = {slab_fma(qfx.xy, fxp), slab_fma(qfx.zw, fxp)};
             const f2 ny[2] = {slab_fma(qny.xy, syp), slab_fma(qny.zw, syp)};
             const f2 fy[2] = {slab_fma(qfy.xy, fyp), slab_fma(qfy.zw, fyp)};
             const f2 nz[2] = {slab_fma(qnz.xy, szp), slab_fma(qnz.zw, szp)};
             const f2 fz[2] = {slab_fma(qfz.xy, fzp), slab_fma(qfz.zw, fzp)};
+#if YK_CULL_BLOCK
+            // two slots per asm block (yk_slab.hpp slab_cull2): the same instructions, fewer edges
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              float tna, tfa, tnb, tfb;
+              slab_cull2(nx[h][0], ny[h][0], nz[h][0], fx[h][0], fy[h][0], fz[h][0], nx[h][1], ny[h][1], nz[h][1],
+                         fx[h][1], fy[h][1], fz[h][1], tmin_lo, ustar_f, tna, tfa, tnb, tfb);
+              hk[2 * h] = tna <= tfa;
+              hk[2 * h + 1] = tnb <= tfb;
+            }
+#else
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const float tn = slab_max(slab_max3(nx[k >> 1][k & 1], ny[k >> 1][k & 1], nz[k >> 1][k & 1]), tmin_lo);
               const float tf = slab_min(slab_min3(fx[k >> 1][k & 1], fy[k >> 1][k & 1], fz[k >> 1][k & 1]), ustar_f);
               hk[k] = tn <= tf;
             }
+#endif
 #else
             const f2 nx[2] = {__builtin_elementwise_fma(qnx.xy, ixv, noix), __builtin_elementwise_fma(qnx.zw, ixv, noix)};
             const f2 fx[2] = {__builtin_elementwise_fma(qfx.xy, ixc, noixc), __builtin_elementwise_fma(qfx.zw, ixc, noixc)};
@@ -1345,7 +1403,13 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
               if (!(lb <= ustar)) continue;
               if (ub < ustar) {
                 ustar = ub;
+#if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
+                // s (RN(ub)(1 + 2^-18) - tmin_lo), rounded up by the factor 1 + 2^-22: >= s (the
+                // unshifted bound - tmin_lo), positive (ub >= t_min > tmin_lo)
+                ustar_f = ((float)ub * (1.0f + 0x1p-18f) - tmin_lo) * ((1.0f + 0x1p-22f) * kClampScale);
+#else
                 ustar_f = (float)ub * (1.0f + 0x1p-18f);
+#endif
               }
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
@@ -1364,7 +1428,13 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
                 // U* >= 0, and lb <= U* implies RN(lb) <= RN(U*) <= ustar_f (monotone rounding),
                 // so the list still keeps every sphere that can be the minimum
                 c3 = c2, l3 = l2, c2 = c1, l2 = l1, c1 = c0, l1 = l0;
+#if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
+                // the same monotone map as ustar_f's: s RN(RN(lb) - tmin_lo) (one FMA, s a power of
+                // two), so lb <= U* still implies l0 <= ustar_f
+                c0 = id, l0 = __builtin_fmaf((float)lb, kClampScale, -tmin_lo * kClampScale);
+#else
                 c0 = id, l0 = (float)lb;
+#endif
                 ++nc;
               } else {
                 nc = 5;  // the list is full: overflow (the exact linear scan decides)
