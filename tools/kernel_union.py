@@ -12,7 +12,7 @@ launch size, also union_per_launch_equiv_ms = union / (spp_total / spp_per_launc
 run mixes synced calls (launches of 4, 8, 16, 32 spp) and back-to-back ones (64 each, round 6), so
 this is the figure comparable with the bench's per-launch launch_ms.
 With last_launches, also union_last_call_per_launch_ms: the union of the last that many dispatches
-(the traced run's last call, in flight like the bench's timed steps after the first) / that many.
+(the traced run's last call, started in flight, its last launch draining alone) / that many.
 Several substrings ('|'-separated) take the union of all their dispatches (kernels that share a
 launch); "launches" = the dispatches of the LAST substring (one per launch).
 """
