@@ -2629,6 +2629,12 @@ constexpr uint64_t kLaunchSlots = YK_LAUNCH_SLOTS;
 #define YK_LAUNCH_SLOTS_OV (1u << 27)
 #endif
 constexpr uint64_t kLaunchSlotsOv = YK_LAUNCH_SLOTS_OV;
+// (A/B) an in-flight call of one launch keeps the rings' full depth, so consecutive one-launch calls
+// overlap like the launches of one call, and the floor of two launches goes
+#ifndef YK_INFLIGHT_DEEP
+#define YK_INFLIGHT_DEEP 0
+#endif
+constexpr bool kInflightDeep = YK_INFLIGHT_DEEP != 0;
 // global launch numbers whose dependency events (ykgpu_context::gev) are kept: more than any ring
 // is deep
 constexpr uint32_t kDepRing = 16;
@@ -2842,7 +2848,9 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
   // (in flight: never fewer than two launches where a synced call has two — a one-launch call has
   // rings of one buffer and overlaps nothing: the 8-way tile 19.6 -> 25.5 ms, r06ad)
   const uint64_t call_launches = launches_for(launch_slots);
-  const uint64_t call_launches_ov = std::max(std::min<uint64_t>(call_launches, 2), launches_for(std::max(launch_slots, kLaunchSlotsOv)));
+  const uint64_t call_launches_ov =
+      kInflightDeep ? launches_for(std::max(launch_slots, kLaunchSlotsOv))
+                    : std::max(std::min<uint64_t>(call_launches, 2), launches_for(std::max(launch_slots, kLaunchSlotsOv)));
   const uint64_t slot_spp = (spp + call_launches - 1) / call_launches;
   const uint64_t slot_spp_ov = (spp + call_launches_ov - 1) / call_launches_ov;
   // A long call takes longer launches: every launch pays a drain whose length is the longest path
@@ -2944,13 +2952,13 @@ int launch(ykgpu_context* ctx, const yk_render_params* p, uint8_t* rgb_dev, doub
     // rings as deep as kWarmRingDepth / col_ring() whatever the call's launch count (a call of two
     // launches reuses the buffers of the call before it, launch() `ov`); one buffer each for a
     // single-launch call
-    kWarmRing = nlaunch > 1 ? kWarmRingDepth : 1;
+    kWarmRing = nlaunch > 1 || (kInflightDeep && inflight) ? kWarmRingDepth : 1;
     if (const char* e = ab_knob("YKGPU_WARM_RING"))  // (A/B) launch buffers in the ring
       kWarmRing = (uint32_t)std::min<uint64_t>(kDepRing - 1, (uint64_t)std::max(2, std::atoi(e)));
     if (warm_first) kWarmRing = nlaunch;
     // colour buffers: render c writes buffer c % ring and waits for the reduce of launch c - ring;
     // reduce c (stream red) overlaps the renders after it
-    kColRing = nlaunch > 1 ? std::min(col_ring(), kDepRing - 1) : 1;
+    kColRing = nlaunch > 1 || (kInflightDeep && inflight) ? std::min(col_ring(), kDepRing - 1) : 1;
     const size_t need_warm = x128 ? 0 : (size_t)kWarmRing * nps * K * welem;
     const size_t need_col = (size_t)kColRing * nps * K * kColStride * sizeof(double);
     if (kmax > kfloor && (need_warm > ctx->warm_cap || need_col > ctx->col_cap * sizeof(double))) {
