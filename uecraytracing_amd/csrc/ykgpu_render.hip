@@ -149,6 +149,10 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 // the FP64 stack sized to the tree's proven depth (3 x wide depth + 1 entries) where LDS allows,
 // its overflow check then skipped (a scalar branch on KernelArgs::stack_check): bench 159.0 ->
 // 156.2 ms on top of YK_NODE_BF (0: always checked, A/B)
+// the FP64 visit's loop in two copies, with and without the stack check (A/B)
+#ifndef YK_VISIT_UNSWITCH
+#define YK_VISIT_UNSWITCH 0
+#endif
 // the FP64 visit's distances from tmin_lo, scaled by kClampScale, the near FMAs clamping to [0, 1]
 // in place of the max with tmin_lo: 4 VALU fewer per visit, bench 150.0 -> 147.0 ms, node visits
 // unchanged, bit-exact (profiles/r06_ab/shade/r06ai_*)
@@ -1223,6 +1227,10 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
 #if YK_NODE_BF
            // the lane's run of interior nodes as a loop of its own tested at the bottom: its exit
            // value is the visit's own result, so the compiler keeps node / top / nc in place
+#if YK_VISIT_UNSWITCH
+           // (two copies of the loop, with and without the stack check: no uniform branch inside)
+           auto visit_run = [&](auto chk) __attribute__((always_inline)) {
+#endif
            do {
 #endif
             if (kCount) ++n_node;
@@ -1323,7 +1331,11 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
               top += (hk[2] && hk[3]) ? kBlk * 4u : (any ? 0u : 0u - kBlk * 4u);
               // stack full: the top stays at the capacity and nc = 5 sends the lane to the scan
               // (only where the plan could not give the stack its proven depth: ka.stack_check)
+#if YK_VISIT_UNSWITCH
+              if (decltype(chk)::value) {
+#else
               if (ka.stack_check) {
+#endif
                 asm volatile("");  // (a scalar branch: no selects on the uniform flag)
                 // signed: with YK_NODE_BF 2 the pop of the sentinel leaves `top` one entry below the
                 // stack's base, below LDS address 0 for the low lanes of a scene with a small LDS
@@ -1333,6 +1345,10 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
               }
             }
            } while (node >= 0);
+#if YK_VISIT_UNSWITCH
+           };
+           if (ka.stack_check) visit_run(std::true_type{}); else visit_run(std::false_type{});
+#endif
 #else
             if (hk[0] || hk[1] || hk[2] || hk[3]) {
               // the last slot entered is visited next and the others entered are pushed, in slot
