@@ -149,6 +149,12 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 // the FP64 stack sized to the tree's proven depth (3 x wide depth + 1 entries) where LDS allows,
 // its overflow check then skipped (a scalar branch on KernelArgs::stack_check): bench 159.0 ->
 // 156.2 ms on top of YK_NODE_BF (0: always checked, A/B)
+// the newest candidate's hb and disc kept from its leaf test, so its exact root skips the second
+// discriminant (17 FP64 operations): bench -0.4...-0.6%, synced -0.6%, the headline image's hash
+// unchanged, no spill at 112 VGPRs (profiles/r06_ab/shade/r06ar_*)
+#ifndef YK_CAND_HD
+#define YK_CAND_HD 1
+#endif
 // the FP64 visit's loop in two copies, with and without the stack check (A/B)
 #ifndef YK_VISIT_UNSWITCH
 #define YK_VISIT_UNSWITCH 0
@@ -411,6 +417,8 @@ __device__ __forceinline__ double root_div(double n, double a, double ra, bool a
   if (__builtin_expect(__ballot(!(a_ok && ykd::num_range(n))) != 0, 0)) q = n / a;
   return q;
 }
+__device__ __forceinline__ void exact_root(uint32_t i, double hb, double disc, double a, double ra, bool a_ok,
+                                           double tmin, Hit& best);
 __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ geo, uint32_t i,
                                                 v3 o, v3 d, double a, double ra, bool a_ok,
                                                 double tmin, Hit& best) {
@@ -419,6 +427,11 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
   const double hb = ykd::dot(oc, d);
   const double c = ykd::len2(oc) - sg.rr;
   const double disc = hb * hb - a * c;
+  exact_root(i, hb, disc, a, ra, a_ok, tmin, best);
+}
+// the root of a candidate whose hb and disc (the reference's, bit for bit) are already known
+__device__ __forceinline__ void exact_root(uint32_t i, double hb, double disc, double a, double ra, bool a_ok,
+                                           double tmin, Hit& best) {
   if (disc < 0) return;  // never taken: the candidate passed the same test
   ++best.sqrts;
   const double sq = ykd::nsqrt_c(disc, best.ncalls, best.nits);
@@ -1196,6 +1209,11 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
         // a lane whose 1/d could leave float's normal range once scaled (|d| >= 1e30, never seen)
         // is marked for the exact linear scan from the start (nc = 5, as an overflow)
         uint32_t nc = dmax < 1e30f ? 0u : 5u, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#if YK_CAND_HD
+        // hb and disc of entry 0 (always the newest candidate: a compaction is followed by the
+        // insertion that caused it), so its exact root needs no second discriminant
+        double hb0 = 0, disc0 = 0;
+#endif
 #else
         uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
 #endif
@@ -1445,6 +1463,9 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
                 // U* >= 0, and lb <= U* implies RN(lb) <= RN(U*) <= ustar_f (monotone rounding),
                 // so the list still keeps every sphere that can be the minimum
                 c3 = c2, l3 = l2, c2 = c1, l2 = l1, c1 = c0, l1 = l0;
+#if YK_CAND_HD
+                hb0 = hb, disc0 = disc;
+#endif
 #if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
                 // the same monotone map as ustar_f's: s RN(RN(lb) - tmin_lo) (one FMA, s a power of
                 // two), so lb <= U* still implies l0 <= ustar_f
@@ -1478,7 +1499,11 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
           // candidate of a ray, so its refined reciprocal is computed once
           const bool a_ok = ykd::div_range(a);
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
+#if YK_CAND_HD
+          if (nc > 0 && l0 <= ustar_f) exact_root(c0, hb0, disc0, a, ra, a_ok, ka.t_min, hit);
+#else
           if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
+#endif
           if (nc > 1 && l1 <= ustar_f) exact_candidate(geo, c1, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 2 && l2 <= ustar_f) exact_candidate(geo, c2, o, d, a, ra, a_ok, ka.t_min, hit);
           if (nc > 3 && l3 <= ustar_f) exact_candidate(geo, c3, o, d, a, ra, a_ok, ka.t_min, hit);
