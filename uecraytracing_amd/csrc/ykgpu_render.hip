@@ -149,6 +149,10 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 // the FP64 stack sized to the tree's proven depth (3 x wide depth + 1 entries) where LDS allows,
 // its overflow check then skipped (a scalar branch on KernelArgs::stack_check): bench 159.0 ->
 // 156.2 ms on top of YK_NODE_BF (0: always checked, A/B)
+// the candidates' refined 1/a from the bounds' 1/a (one Newton step instead of rcp + two; A/B)
+#ifndef YK_RA_FROM_IA
+#define YK_RA_FROM_IA 0
+#endif
 // the newest candidate's hb and disc kept from its leaf test, so its exact root skips the second
 // discriminant (17 FP64 operations): bench -0.4...-0.6%, synced -0.6%, the headline image's hash
 // unchanged, no spill at 112 VGPRs (profiles/r06_ab/shade/r06ar_*)
@@ -1498,7 +1502,13 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
           // exact evaluation of the survivors; the roots' divisor a is the same for every
           // candidate of a ray, so its refined reciprocal is computed once
           const bool a_ok = ykd::div_range(a);
+#if YK_RA_FROM_IA
+          // rcp_refined(a)'s first Newton step is rcp_bound(a) = ia, bit for bit (the same rcp and
+          // fmas): the second step alone (YK_RA_FROM_IA)
+          const double ra = (nc > 0 && a_ok) ? __builtin_fma(ia, __builtin_fma(-a, ia, 1.0), ia) : 0.0;
+#else
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
+#endif
 #if YK_CAND_HD
           if (nc > 0 && l0 <= ustar_f) exact_root(c0, hb0, disc0, a, ra, a_ok, ka.t_min, hit);
 #else
