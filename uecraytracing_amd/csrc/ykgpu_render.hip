@@ -149,6 +149,11 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 // the FP64 stack sized to the tree's proven depth (3 x wide depth + 1 entries) where LDS allows,
 // its overflow check then skipped (a scalar branch on KernelArgs::stack_check): bench 159.0 ->
 // 156.2 ms on top of YK_NODE_BF (0: always checked, A/B)
+// the FP64 candidate list's ids as 16-bit halves of two registers (A/B; written for the
+// YK_CAND_HD / YK_NEAR_CLAMP kernel)
+#ifndef YK_CAND_PACK
+#define YK_CAND_PACK 0
+#endif
 // the candidates' refined 1/a from the bounds' 1/a (one Newton step instead of rcp + two; A/B)
 #ifndef YK_RA_FROM_IA
 #define YK_RA_FROM_IA 0
@@ -1212,7 +1217,13 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
 #if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
         // a lane whose 1/d could leave float's normal range once scaled (|d| >= 1e30, never seen)
         // is marked for the exact linear scan from the start (nc = 5, as an overflow)
+#if YK_CAND_PACK
+        // the candidates' tuple ids as 16-bit halves (ids are < 2^16: ykgpu_set_scene's limit),
+        // entry 0 in cp01's low half
+        uint32_t nc = dmax < 1e30f ? 0u : 5u, cp01 = 0, cp23 = 0;
+#else
         uint32_t nc = dmax < 1e30f ? 0u : 5u, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#endif
 #if YK_CAND_HD
         // hb and disc of entry 0 (always the newest candidate: a compaction is followed by the
         // insertion that caused it), so its exact root needs no second discriminant
@@ -1452,13 +1463,22 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
               }
               if (nc == 4) {  // compact: drop entries the new bound has excluded
                 uint32_t m2 = 0;
+#if YK_CAND_PACK
+                uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+                const uint32_t d0 = cp01 & 0xffffu, d1 = cp01 >> 16, d2 = cp23 & 0xffffu, d3 = cp23 >> 16;
+#else
                 uint32_t d0 = c0, d1 = c1, d2 = c2, d3 = c3;
+#endif
                 float e0 = l0, e1 = l1, e2 = l2, e3 = l3;
                 if (e0 <= ustar_f) { YK_CAND_SET(m2, d0, e0); ++m2; }
                 if (e1 <= ustar_f) { YK_CAND_SET(m2, d1, e1); ++m2; }
                 if (e2 <= ustar_f) { YK_CAND_SET(m2, d2, e2); ++m2; }
                 if (e3 <= ustar_f) { YK_CAND_SET(m2, d3, e3); ++m2; }
                 nc = m2;
+#if YK_CAND_PACK
+                cp01 = c0 | (c1 << 16);
+                cp23 = c2 | (c3 << 16);
+#endif
               }
               if (nc < 4) {
                 // shifted in at entry 0 — straight-line moves instead of a branch per list
@@ -1466,14 +1486,24 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
                 // RN(lb), not rounded down: t_min >= 0 (checked by the host) makes every lb and
                 // U* >= 0, and lb <= U* implies RN(lb) <= RN(U*) <= ustar_f (monotone rounding),
                 // so the list still keeps every sphere that can be the minimum
+#if YK_CAND_PACK
+                cp23 = __builtin_amdgcn_alignbit(cp23, cp01, 16u);  // (cp23 << 16) | (cp01 >> 16)
+                cp01 = (cp01 << 16) | id;
+                l3 = l2, l2 = l1, l1 = l0;
+#else
                 c3 = c2, l3 = l2, c2 = c1, l2 = l1, c1 = c0, l1 = l0;
+#endif
 #if YK_CAND_HD
                 hb0 = hb, disc0 = disc;
 #endif
 #if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
                 // the same monotone map as ustar_f's: s RN(RN(lb) - tmin_lo) (one FMA, s a power of
                 // two), so lb <= U* still implies l0 <= ustar_f
+#if YK_CAND_PACK
+                l0 = __builtin_fmaf((float)lb, kClampScale, -tmin_lo * kClampScale);
+#else
                 c0 = id, l0 = __builtin_fmaf((float)lb, kClampScale, -tmin_lo * kClampScale);
+#endif
 #else
                 c0 = id, l0 = (float)lb;
 #endif
@@ -1510,6 +1540,9 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
           const double ra = (nc > 0 && a_ok) ? ykd::rcp_refined(a) : 0.0;
 #endif
 #if YK_CAND_HD
+#if YK_CAND_PACK
+          const uint32_t c0 = cp01 & 0xffffu, c1 = cp01 >> 16, c2 = cp23 & 0xffffu, c3 = cp23 >> 16;
+#endif
           if (nc > 0 && l0 <= ustar_f) exact_root(c0, hb0, disc0, a, ra, a_ok, ka.t_min, hit);
 #else
           if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
