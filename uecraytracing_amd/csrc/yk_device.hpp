@@ -96,20 +96,19 @@ __device__ __forceinline__ double div_markstein(double n, double d, double y) {
 // Bounds-only approximations (the BVH's root bounds; never a result):
 // v_rsq_f64 / v_rcp_f64 are within 2^-23 (ISA: 2^29 ulp; measured 2^-24.2), one Newton step
 // squares that: relative error < 2^-44.
-__device__ __forceinline__ double sqrt_bound(double x) {  // x >= 0
-  const double r = __builtin_amdgcn_rsq(x);
+__device__ __forceinline__ double sqrt_bound_r(double x, double r) {  // x >= 0, r = rsq(x)
   const double y = x * r, h = 0.5 * r;
   const double y1 = __builtin_fma(__builtin_fma(-y, y, x), h, y);
   return x == 0.0 ? 0.0 : y1;
 }
+__device__ __forceinline__ double sqrt_bound(double x) { return sqrt_bound_r(x, __builtin_amdgcn_rsq(x)); }
 __device__ __forceinline__ double rcp_bound(double a) {  // a > 0
   const double r0 = __builtin_amdgcn_rcp(a);
   return __builtin_fma(r0, __builtin_fma(-a, r0, 1.0), r0);
 }
 // Start of math::sqrt's loop (any start gives the same fixed point; this one is the library's
 // correctly rounded sqrt without its denormal rescaling, valid for s in [2^-400, 2^400]).
-__device__ __forceinline__ double sqrt_start(double s) {
-  const double r = __builtin_amdgcn_rsq(s);
+__device__ __forceinline__ double sqrt_start_r(double s, double r) {  // r = rsq(s), given
   double g = s * r, h = r * 0.5;
   const double e = __builtin_fma(-h, g, 0.5);
   g = __builtin_fma(g, e, g);
@@ -119,8 +118,9 @@ __device__ __forceinline__ double sqrt_start(double s) {
   d = __builtin_fma(-g, g, s);
   return __builtin_fma(d, h, g);
 }
+__device__ __forceinline__ double sqrt_start(double s) { return sqrt_start_r(s, __builtin_amdgcn_rsq(s)); }
 
-__device__ __forceinline__ double nsqrt_impl(double s, uint32_t& iters) {
+__device__ __forceinline__ double nsqrt_impl(double s, uint32_t& iters, const double* rsq = nullptr) {
   double x, prev = 0.0;
   if (s >= 0x1p-400 && s <= 0x1p400) {
     // ONE step from r = RN(sqrt(s)) lands on the loop's fixed point: in ulps of r,
@@ -129,7 +129,7 @@ __device__ __forceinline__ double nsqrt_impl(double s, uint32_t& iters) {
     // reference loop on 4.2e8 values (every s = 2^k +- m ulp, |k| <= 400, m < 2e5, and 1e8
     // random) and by tests/test_oracle_golden.py.  (The division needs no special-case steps
     // for iterates within [2^-201, 2^201].)
-    x = sqrt_start(s);
+    x = rsq ? sqrt_start_r(s, *rsq) : sqrt_start(s);  // (rsq: the same v_rsq_f64 of s, computed before)
     ++iters;
     return (x + div_pos(s, x, rcp_refined(x))) / 2.0;
   }
@@ -150,6 +150,10 @@ __device__ __forceinline__ double nsqrt(double s) {
 __device__ __forceinline__ double nsqrt_c(double s, uint32_t& calls, uint32_t& iters) {
   ++calls;
   return nsqrt_impl(s, iters);
+}
+__device__ __forceinline__ double nsqrt_c_r(double s, double rsq, uint32_t& calls, uint32_t& iters) {
+  ++calls;
+  return nsqrt_impl(s, iters, &rsq);
 }
 
 __device__ __forceinline__ v3 normalized(v3 a) { return divs(a, nsqrt(len2(a))); }  // :127,132

@@ -154,6 +154,10 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 #ifndef YK_CAND_PACK
 #define YK_CAND_PACK 0
 #endif
+// ... and its v_rsq_f64, which math::sqrt's start repeats (A/B; 2 VGPRs more)
+#ifndef YK_CAND_RSQ
+#define YK_CAND_RSQ 0
+#endif
 // the candidates' refined 1/a from the bounds' 1/a (one Newton step instead of rcp + two; A/B)
 #ifndef YK_RA_FROM_IA
 #define YK_RA_FROM_IA 0
@@ -427,7 +431,7 @@ __device__ __forceinline__ double root_div(double n, double a, double ra, bool a
   return q;
 }
 __device__ __forceinline__ void exact_root(uint32_t i, double hb, double disc, double a, double ra, bool a_ok,
-                                           double tmin, Hit& best);
+                                           double tmin, Hit& best, const double* rsq = nullptr);
 __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ geo, uint32_t i,
                                                 v3 o, v3 d, double a, double ra, bool a_ok,
                                                 double tmin, Hit& best) {
@@ -440,10 +444,11 @@ __device__ __forceinline__ void exact_candidate(const SphereGeo* __restrict__ ge
 }
 // the root of a candidate whose hb and disc (the reference's, bit for bit) are already known
 __device__ __forceinline__ void exact_root(uint32_t i, double hb, double disc, double a, double ra, bool a_ok,
-                                           double tmin, Hit& best) {
+                                           double tmin, Hit& best, const double* rsq) {
   if (disc < 0) return;  // never taken: the candidate passed the same test
   ++best.sqrts;
-  const double sq = ykd::nsqrt_c(disc, best.ncalls, best.nits);
+  // (rsq: v_rsq_f64 of this disc from the leaf test, the instruction math::sqrt's start would repeat)
+  const double sq = rsq ? ykd::nsqrt_c_r(disc, *rsq, best.ncalls, best.nits) : ykd::nsqrt_c(disc, best.ncalls, best.nits);
   double r = root_div(-hb - sq, a, ra, a_ok);
   if (r < tmin) {
     r = root_div(-hb + sq, a, ra, a_ok);
@@ -1228,6 +1233,9 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
         // hb and disc of entry 0 (always the newest candidate: a compaction is followed by the
         // insertion that caused it), so its exact root needs no second discriminant
         double hb0 = 0, disc0 = 0;
+#if YK_CAND_RSQ
+        double rsq0 = 0;  // ... and its v_rsq_f64
+#endif
 #endif
 #else
         uint32_t nc = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
@@ -1444,7 +1452,12 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
               if (kCount) ++n_dpos;
               YK_STAMP_DISC_POS();
               // bounds of the exact root: |approx - exact| <= m (256x the error bound, §4)
+#if YK_CAND_HD && YK_CAND_RSQ
+              const double rq = __builtin_amdgcn_rsq(disc);
+              const double sq = ykd::sqrt_bound_r(disc, rq);
+#else
               const double sq = ykd::sqrt_bound(disc);
+#endif
               const double r1 = (-hb - sq) * ia, r2 = (-hb + sq) * ia;
               const double m = (fabs(hb) + sq) * ia * 0x1p-34 + 0x1p-1000;
               if (r2 + m < ka.t_min) continue;  // both roots certainly behind t_min
@@ -1495,6 +1508,9 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
 #endif
 #if YK_CAND_HD
                 hb0 = hb, disc0 = disc;
+#if YK_CAND_RSQ
+                rsq0 = rq;
+#endif
 #endif
 #if YK_SLAB_PAIRS_F64 && YK_NEAR_CLAMP
                 // the same monotone map as ustar_f's: s RN(RN(lb) - tmin_lo) (one FMA, s a power of
@@ -1543,7 +1559,11 @@ __device__ __forceinline__ void render_body(KernelArgs ka) {
 #if YK_CAND_PACK
           const uint32_t c0 = cp01 & 0xffffu, c1 = cp01 >> 16, c2 = cp23 & 0xffffu, c3 = cp23 >> 16;
 #endif
+#if YK_CAND_RSQ
+          if (nc > 0 && l0 <= ustar_f) exact_root(c0, hb0, disc0, a, ra, a_ok, ka.t_min, hit, &rsq0);
+#else
           if (nc > 0 && l0 <= ustar_f) exact_root(c0, hb0, disc0, a, ra, a_ok, ka.t_min, hit);
+#endif
 #else
           if (nc > 0 && l0 <= ustar_f) exact_candidate(geo, c0, o, d, a, ra, a_ok, ka.t_min, hit);
 #endif
