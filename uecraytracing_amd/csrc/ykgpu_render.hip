@@ -149,10 +149,11 @@ constexpr uint32_t kStackRegs = 8;  // attenuation ids kept in registers (4 x 2 
 // the FP64 stack sized to the tree's proven depth (3 x wide depth + 1 entries) where LDS allows,
 // its overflow check then skipped (a scalar branch on KernelArgs::stack_check): bench 159.0 ->
 // 156.2 ms on top of YK_NODE_BF (0: always checked, A/B)
-// the FP64 candidate list's ids as 16-bit halves of two registers (A/B; written for the
-// YK_CAND_HD / YK_NEAR_CLAMP kernel)
+// the FP64 candidate list's ids as 16-bit halves of two registers (written for the YK_CAND_HD /
+// YK_NEAR_CLAMP kernel): the shift-in is one alignbit and one lshl_or instead of four moves, two
+// VGPRs freed; bench -0.3...-0.6%, synced -0.4...-0.8%, image hash unchanged (r06_ab/shade/r06ax_*)
 #ifndef YK_CAND_PACK
-#define YK_CAND_PACK 0
+#define YK_CAND_PACK 1
 #endif
 // ... and its v_rsq_f64, which math::sqrt's start repeats (A/B; 2 VGPRs more)
 #ifndef YK_CAND_RSQ
